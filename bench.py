@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident RS(10,4) encode + reconstruct, 1 MiB shards.
+
+One step = encode a 4096-stripe batch (BASELINE configs[1]) + reconstruct the
+4 erased data shards {0,1,2,3} of every stripe of that batch (configs[2]),
+inputs resident in HBM. N GPUs (torchrun) = N independent stripe batches, one
+per rank (configs[3]: 4096 stripes per GPU, weak scaling, no data-path
+collective; the only collectives are the timing barrier and max).
+
+value = user data processed by the step (k*shard_bytes per stripe for the
+encode plus the same for the reconstruct) / step time, GiB/s, all ranks.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reed-solomon-cc_amd"))
+import reedsol_amd as R  # noqa: E402  (after torch: one HIP runtime)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--shard-bytes", type=int, default=1 << 20)
+    ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU")
+    ap.add_argument("--erase", type=str, default="0,1,2,3", help="erased original indices")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg (0 = skip)")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(k, m, sb, erase, budget_s):
+    """Oracle (C restatement of the reference engine, AVX2 pshufb) on the host
+    cores: the same step (encode + reconstruct) on a bounded stripe sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    present = np.ones(k + m, np.uint8)
+    present[erase] = 0
+    rng = np.random.default_rng(7)
+
+    def run(n_stripes, thr):
+        data = rng.integers(0, 256, (n_stripes, k, sb), dtype=np.uint8)
+        t0 = time.perf_counter()
+        par = O.encode_batch(k, m, data, threads=thr)
+        t1 = time.perf_counter()
+        O.reconstruct_batch(k, m, present, np.concatenate([data, par], axis=1), threads=thr)
+        t2 = time.perf_counter()
+        return n_stripes, t1 - t0, t2 - t1
+
+    # calibrate on one stripe single-threaded, then size both legs to the budget
+    _, te, tr = run(1, 1)
+    per_stripe = te + tr
+    n1 = max(1, int(budget_s * 0.3 / per_stripe))
+    n1 = min(n1, 32)
+    s1, e1, r1 = run(n1, 1)
+    nt = max(threads, int(budget_s * 0.6 / per_stripe * threads))
+    nt = min(nt, 64)
+    st, et, rt = run(nt, threads)
+    gib = k * sb / 2**30
+    return {
+        "value": round(2 * gib * st / (et + rt), 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"RS({k},{m}) {sb >> 10} KiB shards, {st} stripes encode + reconstruct {len(erase)} erased, "
+                  f"{threads} threads (oracle/rs_oracle.c AVX2 engine)",
+        "single_thread": {"value": round(2 * gib * s1 / (e1 + r1), 3), "cores": 1,
+                          "encode_GiBps": round(gib * s1 / e1, 3), "reconstruct_GiBps": round(gib * s1 / r1, 3),
+                          "sample_stripes": s1},
+        "encode_GiBps": round(gib * st / et, 3),
+        "reconstruct_GiBps": round(gib * st / rt, 3),
+        "cpu_model": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_traffic(kernel_names):
+    """HBM bytes per launch from the committed PMC summary (profiles/traffic.json),
+    written by tools/pmc_traffic.py from separate rocprofv3 --pmc passes."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return {n: t[n] for n in kernel_names if n in t}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    k, m, sb, n = args.k, args.m, args.shard_bytes, args.stripes
+    erase = [int(x) for x in args.erase.split(",") if x != ""]
+    e = len(erase)
+    present = [0 if i in erase else 1 for i in range(k)] + [1] * m
+
+    # synthetic, distinct per rank; resident in HBM before timing
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0000 + rank)
+    data = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8, device=dev, generator=g)
+    parity = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
+    restored = torch.empty((n, e, sb), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        R.encode_batch_dev(k, m, data, parity, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        R.reconstruct_batch_dev(k, m, present, data, parity, restored, stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    enc_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in events]))
+    rec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in events]))
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+
+    ok = None
+    if not args.no_verify:
+        ok = bool(torch.equal(restored, data[:, erase]))
+    if world > 1:
+        okt = torch.tensor([1 if ok in (None, True) else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = None if args.no_verify else bool(okt.item())
+
+    if rank == 0:
+        data_bytes = k * sb * n  # per rank per op
+        gib = 2 * data_bytes * world * args.steps / t / 2**30
+        enc_alg = (k + m) * sb * n  # algorithmic HBM bytes per encode launch
+        rec_alg = (k + e) * sb * n  # k received shards read + e restored written
+        kinds = {"encode": (enc_ms, enc_alg, R.encode_kernel_name(k, m, sb)),
+                 "reconstruct": (rec_ms, rec_alg, R.reconstruct_kernel_name(k, m, sb))}
+        dom = max(kinds, key=lambda x: kinds[x][0])
+        ms, alg, kname = kinds[dom]
+        achieved = alg / (ms * 1e-3) / 1e9
+        traffic = load_traffic([kname])
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                    "traffic": (traffic or {}).get(kname, {}).get("hbm_bytes_per_launch") if traffic else None,
+                    "kernel": kname, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ms, 4),
+                    "per_kernel": {kk: {"kernel": v[2], "avg_ms": round(v[0], 4),
+                                        "achieved_GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 1),
+                                        "frac": round(v[1] / (v[0] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                        "data_GiBps": round(data_bytes / (v[0] * 1e-3) / 2**30, 1)}
+                                   for kk, v in kinds.items()}}
+        cpu = None
+        if args.cpu_seconds > 0:
+            cpu = cpu_baseline(k, m, sb, erase, args.cpu_seconds)
+        out = {
+            "metric": "device-resident encode+reconstruct GiB/s per GPU (RS(10,4), 1 MiB shards); % HBM roofline",
+            "value": round(gib, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint bytes, resident in HBM)",
+            "config": {"workload": f"RS({k},{m}) {sb >> 10} KiB shards, {n}-stripe batch per GPU: encode + "
+                                   f"reconstruct {e} erased data shards {erase}",
+                       "k": k, "m": m, "shard_bytes": sb, "stripes_per_gpu": n, "erased": erase,
+                       "parallelism": f"stripe-sharded x{world} (no data-path collective)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "encode_GiBps": round(data_bytes * world / (enc_ms * 1e-3) / 2**30, 2),
+            "reconstruct_GiBps": round(data_bytes * world / (rec_ms * 1e-3) / 2**30, 2),
+            "verified": ok,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

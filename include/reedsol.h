@@ -1,0 +1,154 @@
+/*
+ * reedsol.h — C ABI of the MI355X-native Reed-Solomon engine (librs_amd.so).
+ *
+ * Drop-in for the encode/decode path of usebeforefree/reed-solomon-cc
+ * (Zig, snapshot 2025-12-12): systematic RS over GF(2^16) in a Cantor basis,
+ * Lin-Chung-Han additive FFT, "high rate" codec. Every entry point cites the
+ * reference interface it replaces (paths relative to the reference repo).
+ * Plain pointers and sizes only; no HIP or torch types in any signature
+ * (a stream is passed as an opaque `void*`, i.e. a hipStream_t or NULL).
+ *
+ * Shard layout: the reference's own — a shard of shard_bytes is L =
+ * shard_bytes/64 chunks of 64 B; in a chunk, bytes [0,32) are the low bytes
+ * and [32,64) the high bytes of 32 GF(2^16) symbols (Generic.zig:152-156,
+ * root.zig:373-383). No transposition anywhere.
+ *
+ * Every function returns an rs_status; none aborts. Results are bit-exact
+ * with the reference algorithm (RS_FLAG_REF_LITERAL reproduces its two
+ * arithmetic/schedule defects D1/D2).
+ */
+#ifndef REEDSOL_AMD_H
+#define REEDSOL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes. 1..11 mirror the Zig error set of root.zig
+ * (TooFewOriginalShards .. Overflow); 12.. are conditions where the
+ * reference panics or that only a device engine can hit. */
+typedef enum rs_status {
+  RS_OK = 0,
+  RS_ERR_TOO_FEW_ORIGINAL_SHARDS = 1,  /* root.zig:20, 139 */
+  RS_ERR_NOT_ENOUGH_SHARDS = 2,        /* root.zig:58, 272 */
+  RS_ERR_INVALID_SHARD_SIZE = 3,       /* root.zig:103, 201 */
+  RS_ERR_UNSUPPORTED_SHARD_COUNT = 4,  /* root.zig:398, 407 */
+  RS_ERR_TOO_MANY_ORIGINAL_SHARDS = 5, /* root.zig:129 */
+  RS_ERR_DIFFERENT_SHARD_SIZE = 6,     /* root.zig:130, 243, 259 */
+  RS_ERR_INVALID_SHARD_INDEX = 7,      /* root.zig:240, 254 */
+  RS_ERR_DUPLICATE_SHARD_INDEX = 8,    /* root.zig:241, 256 */
+  RS_ERR_TOO_MANY_SHARDS = 9,          /* root.zig:242, 258 */
+  RS_ERR_OUT_OF_MEMORY = 10,           /* allocator failure */
+  RS_ERR_OVERFLOW = 11,                /* std.math.ceilPowerOfTwo */
+  RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO") */
+  RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* shard_bytes % 64 != 0: root.zig:385 @panic("TODO") */
+  RS_ERR_INVALID_ARGUMENT = 14,        /* NULL pointer / bad stride */
+  RS_ERR_DEVICE = 15,                  /* HIP runtime error (message: rs_last_error()) */
+  RS_ERR_NO_DEVICE = 16,               /* no gfx950 device visible */
+} rs_status;
+
+/* flags for the *_dev and engine entry points */
+#define RS_FLAG_CORRECTED 0u
+#define RS_FLAG_QUIRK_D1 1u /* Generic.zig:283: t1_hi used for nibble 0 of the hi product */
+#define RS_FLAG_QUIRK_D2 2u /* root.zig:151: `<` drops the last full chunk when k % chunk == 0 */
+#define RS_FLAG_REF_LITERAL (RS_FLAG_QUIRK_D1 | RS_FLAG_QUIRK_D2)
+
+typedef void *rs_stream_t; /* hipStream_t, or NULL for the default stream */
+
+/* ------------------------------------------------------------------ info */
+const char *rs_version(void);
+const char *rs_status_name(int status);  /* "NotEnoughShards", ... (Zig error names) */
+const char *rs_last_error(void);         /* thread-local detail for the last non-OK status */
+/* root.zig:397-415 useHighRate: 1 high rate, 0 low rate, negative = -rs_status */
+int rs_use_high_rate(uint64_t original_count, uint64_t recovery_count);
+
+/* ------------------------------------------- one-shot host API (root.zig:14-84)
+ * Host buffers in, host buffers out; internally H2D -> fused HIP kernel -> D2H.
+ * Generalises the reference's 64-byte-typed result to any shard_bytes % 64 == 0
+ * (defect D6). Caller owns every buffer. */
+
+/* replaces `encode(allocator, original_count, recovery_count, original)` root.zig:14-30.
+ * original[k] -> recovery_out[m] (each shard_bytes). */
+int rs_encode(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+              const uint8_t *const *original, uint8_t *const *recovery_out);
+
+/* replaces `decode(allocator, original_count, recovery_count, original, recovery)` root.zig:32-84.
+ * original[i] / recovery[i] == NULL marks a missing shard. restored_out[k]
+ * receives every original (present ones copied through, root.zig:76-81). */
+int rs_decode(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+              const uint8_t *const *original, const uint8_t *const *recovery, uint8_t *const *restored_out);
+
+/* ----------------------------------------- Encoder object (root.zig:86-174) */
+typedef struct rs_encoder rs_encoder;
+/* Encoder.init root.zig:94-122 */
+int rs_encoder_new(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, rs_encoder **out);
+/* Encoder.addOriginalShard root.zig:128-134 */
+int rs_encoder_add_original_shard(rs_encoder *enc, const uint8_t *shard, size_t len);
+/* Encoder.encode root.zig:136-173: recovery_out[m] receives borrowed pointers
+ * valid until the next encode / rs_encoder_free. */
+int rs_encoder_encode(rs_encoder *enc, const uint8_t **recovery_out);
+/* Encoder.deinit root.zig:124-126 (resets for reuse: rs_encoder_reset) */
+void rs_encoder_free(rs_encoder *enc);
+int rs_encoder_reset(rs_encoder *enc);
+
+/* ----------------------------------------- Decoder object (root.zig:176-336)
+ * The reference keeps these methods private; exposed here with the same checks. */
+typedef struct rs_decoder rs_decoder;
+int rs_decoder_new(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, rs_decoder **out);
+int rs_decoder_add_original_shard(rs_decoder *dec, uint64_t index, const uint8_t *shard, size_t len);
+int rs_decoder_add_recovery_shard(rs_decoder *dec, uint64_t index, const uint8_t *shard, size_t len);
+/* restored_out[k]: borrowed pointers; NULL for originals that were supplied
+ * (the caller has them), restored data for the missing ones. */
+int rs_decoder_decode(rs_decoder *dec, const uint8_t **restored_out);
+void rs_decoder_free(rs_decoder *dec);
+
+/* -------------------------------------------- batched device entry points
+ * Device-resident, asynchronous on `stream`, thread-safe, stateless apart
+ * from a per-(k, m, flags[, erasure pattern]) plan cache. Stripes are
+ * independent; shards of one stripe are contiguous (shard stride =
+ * shard_bytes); a stripe stride of 0 means packed.
+ *   d_original: [n_stripes][k][shard_bytes]  (stride original_stripe_stride)
+ *   d_recovery: [n_stripes][m][shard_bytes]  (stride recovery_stripe_stride) */
+int rs_encode_batch_dev(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, uint64_t n_stripes,
+                        const void *d_original, uint64_t original_stripe_stride, void *d_recovery,
+                        uint64_t recovery_stripe_stride, uint32_t flags, rs_stream_t stream);
+
+/* Reconstruct the missing originals of every stripe; one erasure pattern for
+ * the whole batch. present: host array of k+m flags (originals, then
+ * recovery). Missing slots of d_original/d_recovery are never read.
+ *   d_restored: [n_stripes][e][shard_bytes], e = missing originals, ascending index. */
+int rs_reconstruct_batch_dev(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                             uint64_t n_stripes, const uint8_t *present, const void *d_original,
+                             uint64_t original_stripe_stride, const void *d_recovery,
+                             uint64_t recovery_stripe_stride, void *d_restored, uint64_t restored_stripe_stride,
+                             uint32_t flags, rs_stream_t stream);
+
+/* Which device kernel a configuration runs on ("fused_reg_c4_nv4", "generic", ...). */
+const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
+const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
+
+/* ---------------------------------------- Engine seam (Generic.zig), test shim
+ * The reference's comptime Engine interface (root.zig:10-12) at per-call
+ * granularity, run on the GPU over a HOST buffer of shard_count shards of
+ * shard_bytes (copied in and out). For stage-by-stage parity only. */
+int rs_engine_fft(uint8_t *shards, uint64_t shard_count, size_t shard_bytes, uint64_t pos, uint64_t size,
+                  uint64_t truncated_size, uint64_t skew_delta, uint32_t flags);  /* Generic.zig:15 */
+int rs_engine_ifft(uint8_t *shards, uint64_t shard_count, size_t shard_bytes, uint64_t pos, uint64_t size,
+                   uint64_t truncated_size, uint64_t skew_delta, uint32_t flags); /* Generic.zig:80 */
+int rs_engine_mul_scalar(uint8_t *chunks, size_t bytes, uint16_t log_m, uint32_t flags); /* Generic.zig:220 */
+/* Generic.zig:200 evalPoly over 65536 u16 erasure flags, in place (host FWHT). */
+int rs_engine_eval_poly(uint16_t *erasures, uint64_t truncated_size);
+
+/* ---------------------------------------------------- tables (tables.zig) */
+const uint16_t *rs_table_exp(void);       /* [65536] */
+const uint16_t *rs_table_log(void);       /* [65536] */
+const uint16_t *rs_table_skew(void);      /* [65535] */
+const uint16_t *rs_table_log_walsh(void); /* [65536] */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REEDSOL_AMD_H */

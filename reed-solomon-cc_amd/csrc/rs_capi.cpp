@@ -1,0 +1,689 @@
+// rs_capi.cpp — host codec and C ABI (include/reedsol.h) of librs_amd.so.
+//
+// Host-side mirror of root.zig: argument validation and error precedence of
+// encode/decode/Encoder/Decoder/useHighRate, plan building (butterfly schedule
+// + v_perm tables + erasure-locator evaluation) and kernel launches. Every
+// device computation runs in rs_kernels.hip; there is no CPU compute path —
+// without a gfx950 device the entry points return RS_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/reedsol.h"
+#include "rs_gf.hpp"
+#include "rs_internal.hpp"
+
+using namespace rs;
+
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int status, const std::string &msg) {
+  t_last_error = msg;
+  return status;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  return fail(RS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                               \
+  do {                                              \
+    hipError_t e_ = (expr);                         \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+// ---------------------------------------------------------------- devices
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_ok;  // device -> RS_OK / RS_ERR_NO_DEVICE
+
+int current_device(int *dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RS_ERR_NO_DEVICE, "no HIP device visible");
+  HIP_TRY(hipGetDevice(dev));
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto it = g_dev_ok.find(*dev);
+  if (it == g_dev_ok.end()) {
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, *dev));
+    const bool ok = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    it = g_dev_ok.emplace(*dev, ok ? RS_OK : RS_ERR_NO_DEVICE).first;
+    if (!ok) return fail(RS_ERR_NO_DEVICE, std::string("device arch ") + prop.gcnArchName + " is not gfx950");
+  }
+  if (it->second != RS_OK) return fail(it->second, "device is not gfx950");
+  return RS_OK;
+}
+
+// ------------------------------------------------------------ validation
+// root.zig:397-415
+int use_high_rate(uint64_t original, uint64_t recovery) {
+  if (original > kOrder || recovery > kOrder) return -RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (original == 0 || recovery == 0) return -RS_ERR_UNSUPPORTED_SHARD_COUNT;  // ceilPowerOfTwo(0) asserts
+  const uint64_t op = ceil_pow2(original), rp = ceil_pow2(recovery);
+  const uint64_t smaller = std::min(op, rp), larger = std::max(original, recovery);
+  if (smaller + larger > kOrder) return -RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (op < rp) return 0;
+  if (op > rp) return 1;
+  return original <= recovery ? 1 : 0;
+}
+
+// Encoder.init / Decoder.init checks (root.zig:100-103, 198-201) + the tail panic (root.zig:385)
+int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
+  const int hr = use_high_rate(k, m);
+  if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
+  if (hr == 0) return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec (reference panics, root.zig:120)");
+  if (shard_bytes == 0 || (shard_bytes & 1)) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes is 0 or odd");
+  if (shard_bytes % 64) return fail(RS_ERR_SHARD_TAIL_UNSUPPORTED, "shard_bytes % 64 != 0 (reference panics, root.zig:385)");
+  return RS_OK;
+}
+
+int align_nv(std::initializer_list<uint64_t> vals) {
+  uint64_t a = 0;
+  for (uint64_t v : vals) a |= v;
+  if (a % 16 == 0) return 4;
+  if (a % 8 == 0) return 2;
+  if (a % 4 == 0) return 1;
+  return 0;
+}
+
+// ------------------------------------------------------------------ plans
+struct DevBuf {
+  void *p = nullptr;
+  int dev = 0;
+  ~DevBuf() {
+    if (p) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+      (void)hipSetDevice(cur);
+    }
+  }
+};
+
+struct EncodePlan {
+  std::shared_ptr<DevBuf> buf;
+  uint32_t chunk, n_chunks, trunc_first, trunc_last, tabs_per_chunk, work;
+};
+
+struct DecodePlan {
+  std::shared_ptr<DevBuf> buf;
+  uint32_t work, chunk, trunc, e;
+  size_t off_fft, off_pre, off_post, off_src, off_dst;  // byte offsets into buf
+};
+
+std::mutex g_plan_mu;
+std::map<std::string, std::shared_ptr<EncodePlan>> g_enc_plans;
+std::map<std::string, std::shared_ptr<DecodePlan>> g_dec_plans;
+
+int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out) {
+  auto b = std::make_shared<DevBuf>();
+  b->dev = dev;
+  HIP_TRY(hipMalloc(&b->p, std::max<size_t>(bytes, 16)));
+  HIP_TRY(hipMemcpy(b->p, host, bytes, hipMemcpyHostToDevice));
+  out = b;
+  return RS_OK;
+}
+
+// root.zig:136-173 chunk schedule -> table block
+int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out) {
+  char key[128];
+  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u", dev, (unsigned long long)k, (unsigned long long)m, flags);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_enc_plans.find(key);
+  if (it != g_enc_plans.end()) {
+    out = it->second;
+    return RS_OK;
+  }
+  const bool d1 = flags & RS_FLAG_QUIRK_D1, d2 = flags & RS_FLAG_QUIRK_D2;
+  const uint64_t C = ceil_pow2(m);
+  std::vector<uint64_t> truncs;  // per IFFT chunk, chunk j at position j*C
+  truncs.push_back(std::min(k, C));
+  if (k > C) {
+    uint64_t cs = C;
+    while (d2 ? (cs + C < k) : (cs + C <= k)) {  // root.zig:151 (D2: `<`)
+      truncs.push_back(C);
+      cs += C;
+    }
+    if (k % C) truncs.push_back(k % C);  // root.zig:159-166
+  }
+  std::vector<RsTab> tabs;
+  for (size_t j = 0; j < truncs.size(); j++) push_ifft_tabs(tabs, C, (j + 1) * C, d1);
+  push_fft_tabs(tabs, C, 0, d1);
+  auto plan = std::make_shared<EncodePlan>();
+  int st = upload(tabs.data(), tabs.size() * sizeof(RsTab), dev, plan->buf);
+  if (st) return st;
+  plan->chunk = static_cast<uint32_t>(C);
+  plan->n_chunks = static_cast<uint32_t>(truncs.size());
+  plan->trunc_first = static_cast<uint32_t>(truncs.front());
+  plan->trunc_last = static_cast<uint32_t>(truncs.back());
+  plan->tabs_per_chunk = static_cast<uint32_t>(ifft_tab_count(C));
+  plan->work = static_cast<uint32_t>((k + C - 1) / C * C);
+  g_enc_plans.emplace(key, plan);
+  out = plan;
+  return RS_OK;
+}
+
+// root.zig:268-335 erasure pattern -> evalPoly -> masks and table block
+int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present,
+                    std::shared_ptr<DecodePlan> &out) {
+  std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                    std::to_string(flags) + "/";
+  key.reserve(key.size() + k + m);
+  for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_dec_plans.find(key);
+  if (it != g_dec_plans.end()) {
+    out = it->second;
+    return RS_OK;
+  }
+  const bool d1 = flags & RS_FLAG_QUIRK_D1;
+  const uint64_t C = ceil_pow2(m), end = C + k, W = ceil_pow2(C + k);
+  std::vector<uint8_t> received(W, 0);
+  for (uint64_t i = 0; i < m; i++) received[i] = present[k + i] ? 1 : 0;
+  for (uint64_t i = 0; i < k; i++) received[C + i] = present[i] ? 1 : 0;
+  std::vector<uint16_t> er(kOrder, 0);
+  for (uint64_t i = 0; i < m; i++)  // root.zig:278-287
+    if (!received[i]) er[i] = 1;
+  for (uint64_t i = m; i < C; i++) er[i] = 1;
+  for (uint64_t i = C; i < end; i++)
+    if (!received[i]) er[i] = 1;
+  eval_poly(er.data(), end);  // root.zig:289
+
+  std::vector<RsTab> tabs;
+  push_ifft_tabs(tabs, W, 0, d1);
+  const size_t n_ifft = tabs.size();
+  push_fft_tabs(tabs, W, 0, d1);
+  const size_t n_fft = tabs.size() - n_ifft;
+  std::vector<int32_t> src(W, -1), dst(W, -1);
+  std::vector<RsTab> pre(W), post(W);
+  uint32_t e = 0;
+  for (uint64_t p = 0; p < W; p++) {
+    if (p < m && received[p]) {
+      src[p] = kSrcRecovery | static_cast<int32_t>(p);
+      pre[p] = make_tab(er[p], d1);
+    } else if (p >= C && p < end && received[p]) {
+      src[p] = static_cast<int32_t>(p - C);
+      pre[p] = make_tab(er[p], d1);
+    }
+    if (p >= C && p < end && !received[p]) {
+      dst[p] = static_cast<int32_t>(e++);
+      post[p] = make_tab(static_cast<uint16_t>(kModulus - er[p]), d1);  // root.zig:321-326
+    }
+  }
+  tabs.insert(tabs.end(), pre.begin(), pre.end());
+  tabs.insert(tabs.end(), post.begin(), post.end());
+  std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + 2 * W * sizeof(int32_t));
+  std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
+  const size_t off_src = tabs.size() * sizeof(RsTab), off_dst = off_src + W * sizeof(int32_t);
+  std::memcpy(blob.data() + off_src, src.data(), W * sizeof(int32_t));
+  std::memcpy(blob.data() + off_dst, dst.data(), W * sizeof(int32_t));
+  auto plan = std::make_shared<DecodePlan>();
+  int st = upload(blob.data(), blob.size(), dev, plan->buf);
+  if (st) return st;
+  plan->work = static_cast<uint32_t>(W);
+  plan->chunk = static_cast<uint32_t>(C);
+  plan->trunc = static_cast<uint32_t>(end);
+  plan->e = e;
+  plan->off_fft = n_ifft * sizeof(RsTab);
+  plan->off_pre = (n_ifft + n_fft) * sizeof(RsTab);
+  plan->off_post = plan->off_pre + W * sizeof(RsTab);
+  plan->off_src = off_src;
+  plan->off_dst = off_dst;
+  g_dec_plans.emplace(key, plan);
+  out = plan;
+  return RS_OK;
+}
+
+constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
+
+}  // namespace
+
+// ===================================================================== ABI
+extern "C" {
+
+const char *rs_version(void) { return "rs-amd 0.1.0 (gfx950)"; }
+
+const char *rs_status_name(int s) {
+  static const char *kNames[] = {"Ok",
+                                 "TooFewOriginalShards",
+                                 "NotEnoughShards",
+                                 "InvalidShardSize",
+                                 "UnsupportedShardCount",
+                                 "TooManyOriginalShards",
+                                 "DifferentShardSize",
+                                 "InvalidShardIndex",
+                                 "DuplicateShardIndex",
+                                 "TooManyShards",
+                                 "OutOfMemory",
+                                 "Overflow",
+                                 "LowRateUnsupported",
+                                 "ShardTailUnsupported",
+                                 "InvalidArgument",
+                                 "DeviceError",
+                                 "NoDevice"};
+  if (s < 0 || s >= static_cast<int>(sizeof kNames / sizeof kNames[0])) return "Unknown";
+  return kNames[s];
+}
+
+const char *rs_last_error(void) { return t_last_error.c_str(); }
+
+int rs_use_high_rate(uint64_t k, uint64_t m) { return use_high_rate(k, m); }
+
+const uint16_t *rs_table_exp(void) { return tables().exp; }
+const uint16_t *rs_table_log(void) { return tables().log; }
+const uint16_t *rs_table_skew(void) { return tables().skew; }
+const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
+
+const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) { return choose_encode(k, m, sb, 4).name; }
+const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb) { return choose_decode(k, m, sb, 4).name; }
+
+int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const void *d_original,
+                        uint64_t orig_stride, void *d_recovery, uint64_t rec_stride, uint32_t flags,
+                        rs_stream_t stream) {
+  if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  if (n_stripes == 0) return RS_OK;
+  if (!d_original || !d_recovery) return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
+  if (orig_stride == 0) orig_stride = k * sb;
+  if (rec_stride == 0) rec_stride = m * sb;
+  if (orig_stride < k * sb || rec_stride < m * sb) return fail(RS_ERR_INVALID_ARGUMENT, "stripe stride too small");
+  const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
+                               orig_stride, rec_stride});
+  if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
+  int dev;
+  if ((st = current_device(&dev))) return st;
+  std::shared_ptr<EncodePlan> plan;
+  if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
+  const KernelChoice kc = choose_encode(k, m, sb, max_nv);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  EncodeArgs a{};
+  a.data = static_cast<const uint8_t *>(d_original);
+  a.data_stripe_stride = orig_stride;
+  a.parity = static_cast<uint8_t *>(d_recovery);
+  a.parity_stripe_stride = rec_stride;
+  a.shard_bytes = sb;
+  a.tabs = static_cast<const RsTab *>(plan->buf->p);
+  a.chunk = plan->chunk;
+  a.n_chunks = plan->n_chunks;
+  a.trunc_first = plan->trunc_first;
+  a.trunc_last = plan->trunc_last;
+  a.m = static_cast<uint32_t>(m);
+  a.k = static_cast<uint32_t>(k);
+  a.tabs_per_chunk = plan->tabs_per_chunk;
+  a.work = plan->work;
+  if (kc.variant == Variant::kRegister) {
+    a.n_stripes = n_stripes;
+    HIP_TRY(launch_encode(kc, a, s));
+    return RS_OK;
+  }
+  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
+  void *scratch = nullptr;
+  HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
+  for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
+    EncodeArgs b = a;
+    b.data += s0 * orig_stride;
+    b.parity += s0 * rec_stride;
+    b.n_stripes = std::min(per, n_stripes - s0);
+    b.scratch = static_cast<uint8_t *>(scratch);
+    b.scratch_stripes = per;
+    hipError_t e = launch_encode(kc, b, s);
+    if (e != hipSuccess) {
+      (void)hipFreeAsync(scratch, s);
+      return hip_fail(e, "launch_encode");
+    }
+  }
+  HIP_TRY(hipFreeAsync(scratch, s));
+  return RS_OK;
+}
+
+int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const uint8_t *present,
+                             const void *d_original, uint64_t orig_stride, const void *d_recovery,
+                             uint64_t rec_stride, void *d_restored, uint64_t out_stride, uint32_t flags,
+                             rs_stream_t stream) {
+  if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  uint64_t have = 0, e = 0, have_rec = 0;
+  for (uint64_t i = 0; i < k; i++) {
+    have += present[i] != 0;
+    e += present[i] == 0;
+  }
+  for (uint64_t i = 0; i < m; i++) have_rec += present[k + i] != 0;
+  if (have + have_rec < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+  if (e == 0 || n_stripes == 0) return RS_OK;  // nothing missing: root.zig:48-57 copy-through
+  if (orig_stride == 0) orig_stride = k * sb;
+  if (rec_stride == 0) rec_stride = m * sb;
+  if (out_stride == 0) out_stride = e * sb;
+  if ((have && !d_original) || (have_rec && !d_recovery) || !d_restored)
+    return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
+  const int max_nv =
+      align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
+                reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
+  if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
+  int dev;
+  if ((st = current_device(&dev))) return st;
+  std::shared_ptr<DecodePlan> plan;
+  if ((st = get_decode_plan(dev, k, m, flags, present, plan))) return st;
+  const KernelChoice kc = choose_decode(k, m, sb, max_nv);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint8_t *base = static_cast<const uint8_t *>(plan->buf->p);
+  DecodeArgs a{};
+  a.orig = static_cast<const uint8_t *>(d_original);
+  a.orig_stripe_stride = orig_stride;
+  a.rec = static_cast<const uint8_t *>(d_recovery);
+  a.rec_stripe_stride = rec_stride;
+  a.out = static_cast<uint8_t *>(d_restored);
+  a.out_stripe_stride = out_stride;
+  a.shard_bytes = sb;
+  a.tab_ifft = reinterpret_cast<const RsTab *>(base);
+  a.tab_fft = reinterpret_cast<const RsTab *>(base + plan->off_fft);
+  a.tab_pre = reinterpret_cast<const RsTab *>(base + plan->off_pre);
+  a.tab_post = reinterpret_cast<const RsTab *>(base + plan->off_post);
+  a.pos_src = reinterpret_cast<const int32_t *>(base + plan->off_src);
+  a.pos_dst = reinterpret_cast<const int32_t *>(base + plan->off_dst);
+  a.work = plan->work;
+  a.trunc = plan->trunc;
+  if (!a.orig) a.orig = a.rec;  // never dereferenced for absent shards
+  if (!a.rec) a.rec = a.orig;
+  if (kc.variant == Variant::kRegister) {
+    a.n_stripes = n_stripes;
+    HIP_TRY(launch_decode(kc, a, s));
+    return RS_OK;
+  }
+  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
+  void *scratch = nullptr;
+  HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
+  for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
+    DecodeArgs b = a;
+    b.orig += s0 * orig_stride;
+    b.rec += s0 * rec_stride;
+    b.out += s0 * out_stride;
+    b.n_stripes = std::min(per, n_stripes - s0);
+    b.scratch = static_cast<uint8_t *>(scratch);
+    b.scratch_stripes = per;
+    hipError_t err = launch_decode(kc, b, s);
+    if (err != hipSuccess) {
+      (void)hipFreeAsync(scratch, s);
+      return hip_fail(err, "launch_decode");
+    }
+  }
+  HIP_TRY(hipFreeAsync(scratch, s));
+  return RS_OK;
+}
+
+// ------------------------------------------------------------ one-shot host
+namespace {
+struct DevMem {
+  void *p = nullptr;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+int rs_encode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, uint8_t *const *recovery_out) {
+  if (k == 0 || !original) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "no original shards");  // root.zig:20
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  for (uint64_t i = 0; i < k; i++)
+    if (!original[i]) return fail(RS_ERR_INVALID_ARGUMENT, "NULL original shard");
+  if (!recovery_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL recovery_out");
+  int dev;
+  if ((st = current_device(&dev))) return st;
+  DevMem din, dout;
+  HIP_TRY(hipMalloc(&din.p, k * sb));
+  HIP_TRY(hipMalloc(&dout.p, m * sb));
+  for (uint64_t i = 0; i < k; i++)
+    HIP_TRY(hipMemcpy(static_cast<uint8_t *>(din.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
+  if ((st = rs_encode_batch_dev(k, m, sb, 1, din.p, 0, dout.p, 0, RS_FLAG_CORRECTED, nullptr))) return st;
+  for (uint64_t r = 0; r < m; r++)
+    HIP_TRY(hipMemcpy(recovery_out[r], static_cast<uint8_t *>(dout.p) + r * sb, sb, hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+int rs_decode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, const uint8_t *const *recovery,
+              uint8_t *const *restored_out) {
+  if (!original || !recovery || !restored_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL array");
+  uint64_t orig_present = 0, rec_present = 0;
+  for (uint64_t i = 0; i < k; i++) orig_present += original[i] != nullptr;
+  for (uint64_t i = 0; i < m; i++) rec_present += recovery[i] != nullptr;
+  if (rec_present == 0) {  // root.zig:39-59
+    if (orig_present != k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "no recovery shards and originals incomplete");
+    for (uint64_t i = 0; i < k; i++) std::memcpy(restored_out[i], original[i], sb);
+    return RS_OK;
+  }
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  if (orig_present + rec_present < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");  // root.zig:271
+  std::vector<uint8_t> present(k + m);
+  for (uint64_t i = 0; i < k; i++) present[i] = original[i] != nullptr;
+  for (uint64_t i = 0; i < m; i++) present[k + i] = recovery[i] != nullptr;
+  const uint64_t e = k - orig_present;
+  if (e > 0) {
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    DevMem dorig, drec, dout;
+    HIP_TRY(hipMalloc(&dorig.p, k * sb));
+    HIP_TRY(hipMalloc(&drec.p, m * sb));
+    HIP_TRY(hipMalloc(&dout.p, e * sb));
+    for (uint64_t i = 0; i < k; i++)
+      if (original[i])
+        HIP_TRY(hipMemcpy(static_cast<uint8_t *>(dorig.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
+    for (uint64_t i = 0; i < m; i++)
+      if (recovery[i])
+        HIP_TRY(hipMemcpy(static_cast<uint8_t *>(drec.p) + i * sb, recovery[i], sb, hipMemcpyHostToDevice));
+    if ((st = rs_reconstruct_batch_dev(k, m, sb, 1, present.data(), dorig.p, 0, drec.p, 0, dout.p, 0,
+                                       RS_FLAG_CORRECTED, nullptr)))
+      return st;
+    uint64_t slot = 0;
+    for (uint64_t i = 0; i < k; i++)
+      if (!original[i])
+        HIP_TRY(hipMemcpy(restored_out[i], static_cast<uint8_t *>(dout.p) + (slot++) * sb, sb,
+                          hipMemcpyDeviceToHost));
+  }
+  for (uint64_t i = 0; i < k; i++)  // root.zig:76-81
+    if (original[i]) std::memcpy(restored_out[i], original[i], sb);
+  return RS_OK;
+}
+
+// ---------------------------------------------------------------- Encoder
+struct rs_encoder {
+  uint64_t k, m;
+  size_t sb;
+  uint64_t received = 0;
+  std::vector<uint8_t> originals, recovery;
+};
+
+int rs_encoder_new(uint64_t k, uint64_t m, size_t sb, rs_encoder **out) {
+  if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
+  *out = nullptr;
+  int st = check_codec(k, m, sb);  // root.zig:100-103
+  if (st) return st;
+  try {
+    rs_encoder *e = new rs_encoder;
+    e->k = k;
+    e->m = m;
+    e->sb = sb;
+    e->originals.assign(k * sb, 0);
+    e->recovery.assign(m * sb, 0);
+    *out = e;
+  } catch (...) {
+    return fail(RS_ERR_OUT_OF_MEMORY, "allocation failed");
+  }
+  return RS_OK;
+}
+
+int rs_encoder_add_original_shard(rs_encoder *e, const uint8_t *shard, size_t len) {
+  if (!e || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (e->received == e->k) return fail(RS_ERR_TOO_MANY_ORIGINAL_SHARDS, "too many original shards");  // root.zig:129
+  if (len != e->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");                // root.zig:130
+  std::memcpy(e->originals.data() + e->received * e->sb, shard, len);
+  e->received++;
+  return RS_OK;
+}
+
+int rs_encoder_encode(rs_encoder *e, const uint8_t **recovery_out) {
+  if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
+  if (e->received != e->k) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "too few original shards");  // root.zig:139
+  std::vector<const uint8_t *> in(e->k);
+  std::vector<uint8_t *> out(e->m);
+  for (uint64_t i = 0; i < e->k; i++) in[i] = e->originals.data() + i * e->sb;
+  for (uint64_t i = 0; i < e->m; i++) out[i] = e->recovery.data() + i * e->sb;
+  int st = rs_encode(e->k, e->m, e->sb, in.data(), out.data());
+  if (st) return st;
+  if (recovery_out)
+    for (uint64_t i = 0; i < e->m; i++) recovery_out[i] = out[i];
+  return RS_OK;
+}
+
+int rs_encoder_reset(rs_encoder *e) {
+  if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
+  e->received = 0;
+  return RS_OK;
+}
+
+void rs_encoder_free(rs_encoder *e) { delete e; }
+
+// ---------------------------------------------------------------- Decoder
+struct rs_decoder {
+  uint64_t k, m;
+  size_t sb;
+  uint64_t orig_received = 0, rec_received = 0;
+  std::vector<uint8_t> originals, recovery, restored;
+  std::vector<uint8_t> have_orig, have_rec;
+};
+
+int rs_decoder_new(uint64_t k, uint64_t m, size_t sb, rs_decoder **out) {
+  if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
+  *out = nullptr;
+  int st = check_codec(k, m, sb);  // root.zig:198-201
+  if (st) return st;
+  try {
+    rs_decoder *d = new rs_decoder;
+    d->k = k;
+    d->m = m;
+    d->sb = sb;
+    d->originals.assign(k * sb, 0);
+    d->recovery.assign(m * sb, 0);
+    d->restored.assign(k * sb, 0);
+    d->have_orig.assign(k, 0);
+    d->have_rec.assign(m, 0);
+    *out = d;
+  } catch (...) {
+    return fail(RS_ERR_OUT_OF_MEMORY, "allocation failed");
+  }
+  return RS_OK;
+}
+
+// root.zig:236-248
+int rs_decoder_add_original_shard(rs_decoder *d, uint64_t index, const uint8_t *shard, size_t len) {
+  if (!d || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (index >= d->k) return fail(RS_ERR_INVALID_SHARD_INDEX, "original index out of range");
+  if (d->have_orig[index]) return fail(RS_ERR_DUPLICATE_SHARD_INDEX, "duplicate original index");
+  if (d->orig_received == d->k) return fail(RS_ERR_TOO_MANY_SHARDS, "too many original shards");
+  if (len != d->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");
+  std::memcpy(d->originals.data() + index * d->sb, shard, len);
+  d->have_orig[index] = 1;
+  d->orig_received++;
+  return RS_OK;
+}
+
+// root.zig:250-265
+int rs_decoder_add_recovery_shard(rs_decoder *d, uint64_t index, const uint8_t *shard, size_t len) {
+  if (!d || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
+  if (index >= d->m) return fail(RS_ERR_INVALID_SHARD_INDEX, "recovery index out of range");
+  if (d->have_rec[index]) return fail(RS_ERR_DUPLICATE_SHARD_INDEX, "duplicate recovery index");
+  if (d->rec_received == d->m) return fail(RS_ERR_TOO_MANY_SHARDS, "too many recovery shards");
+  if (len != d->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");
+  std::memcpy(d->recovery.data() + index * d->sb, shard, len);
+  d->have_rec[index] = 1;
+  d->rec_received++;
+  return RS_OK;
+}
+
+// root.zig:268-335; restored_out[i] points at the original (supplied or restored)
+int rs_decoder_decode(rs_decoder *d, const uint8_t **restored_out) {
+  if (!d) return fail(RS_ERR_INVALID_ARGUMENT, "NULL decoder");
+  if (d->orig_received + d->rec_received < d->k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");
+  std::vector<const uint8_t *> o(d->k), r(d->m);
+  std::vector<uint8_t *> out(d->k);
+  for (uint64_t i = 0; i < d->k; i++) {
+    o[i] = d->have_orig[i] ? d->originals.data() + i * d->sb : nullptr;
+    out[i] = d->restored.data() + i * d->sb;
+  }
+  for (uint64_t i = 0; i < d->m; i++) r[i] = d->have_rec[i] ? d->recovery.data() + i * d->sb : nullptr;
+  int st = rs_decode(d->k, d->m, d->sb, o.data(), r.data(), out.data());
+  if (st) return st;
+  if (restored_out)
+    for (uint64_t i = 0; i < d->k; i++) restored_out[i] = out[i];
+  return RS_OK;
+}
+
+void rs_decoder_free(rs_decoder *d) { delete d; }
+
+// ------------------------------------------------------------- engine shims
+static int engine_transform(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size,
+                            uint64_t trunc, uint64_t sd, uint32_t flags, bool inverse) {
+  if (!shards) return fail(RS_ERR_INVALID_ARGUMENT, "NULL shards");
+  if (sb == 0 || sb % 64) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes must be a multiple of 64");
+  if (pos + size > count || trunc > size) return fail(RS_ERR_INVALID_ARGUMENT, "pos/size/trunc out of range");
+  int dev, st;
+  if ((st = current_device(&dev))) return st;
+  std::vector<RsTab> tabs;
+  if (inverse) push_ifft_tabs(tabs, size, sd, flags & RS_FLAG_QUIRK_D1);
+  else push_fft_tabs(tabs, size, sd, flags & RS_FLAG_QUIRK_D1);
+  DevMem dt, dw;
+  HIP_TRY(hipMalloc(&dt.p, std::max<size_t>(16, tabs.size() * sizeof(RsTab))));
+  if (!tabs.empty()) HIP_TRY(hipMemcpy(dt.p, tabs.data(), tabs.size() * sizeof(RsTab), hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&dw.p, count * sb));
+  HIP_TRY(hipMemcpy(dw.p, shards, count * sb, hipMemcpyHostToDevice));
+  HIP_TRY(launch_engine_fft(static_cast<uint8_t *>(dw.p), sb, pos, size, trunc, static_cast<const RsTab *>(dt.p),
+                            inverse, nullptr));
+  HIP_TRY(hipMemcpy(shards, dw.p, count * sb, hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+int rs_engine_fft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
+                  uint64_t sd, uint32_t flags) {
+  return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, false);
+}
+
+int rs_engine_ifft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
+                   uint64_t sd, uint32_t flags) {
+  return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, true);
+}
+
+int rs_engine_mul_scalar(uint8_t *chunks, size_t bytes, uint16_t log_m, uint32_t flags) {
+  if (!chunks) return fail(RS_ERR_INVALID_ARGUMENT, "NULL chunks");
+  if (bytes == 0 || bytes % 64) return fail(RS_ERR_INVALID_SHARD_SIZE, "bytes must be a multiple of 64");
+  int dev, st;
+  if ((st = current_device(&dev))) return st;
+  const RsTab t = make_tab(log_m, flags & RS_FLAG_QUIRK_D1);
+  DevMem dt, dw;
+  HIP_TRY(hipMalloc(&dt.p, sizeof t));
+  HIP_TRY(hipMemcpy(dt.p, &t, sizeof t, hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc(&dw.p, bytes));
+  HIP_TRY(hipMemcpy(dw.p, chunks, bytes, hipMemcpyHostToDevice));
+  HIP_TRY(launch_mul_scalar(static_cast<uint8_t *>(dw.p), bytes, static_cast<const RsTab *>(dt.p), nullptr));
+  HIP_TRY(hipMemcpy(chunks, dw.p, bytes, hipMemcpyDeviceToHost));
+  return RS_OK;
+}
+
+int rs_engine_eval_poly(uint16_t *erasures, uint64_t trunc) {
+  if (!erasures) return fail(RS_ERR_INVALID_ARGUMENT, "NULL erasures");
+  if (trunc > kOrder) return fail(RS_ERR_INVALID_ARGUMENT, "truncated_size > 65536");
+  eval_poly(erasures, trunc);
+  return RS_OK;
+}
+
+}  // extern "C"

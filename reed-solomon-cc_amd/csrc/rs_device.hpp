@@ -1,0 +1,236 @@
+// rs_device.hpp — CDNA4 (gfx950) device primitives for the GF(2^16) additive FFT.
+//
+// Data in registers: a lane owns NV "dword pairs" of one 64-byte chunk column —
+// lo dword j holds the low bytes of 4 symbols (chunk bytes [4j, 4j+4)), hi dword
+// j their high bytes (chunk bytes [32+4j, 32+4j+4)) — the reference's chunk
+// layout (Generic.zig:152-156) read straight from HBM, no transposition.
+//
+// Multiply by a constant (Generic.zig:275-298 `mul`): 6 bit-field selectors per
+// dword pair, 12 v_perm_b32 table lookups (4 symbols each), 6 v_bitop3 XOR3.
+// Twiddle tables (RsTab, 96 B) are wave-uniform: scalar-loaded from the plan.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "rs_gf.hpp"
+
+namespace rs {
+namespace dev {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// v_perm_b32: byte i of result = byte sel.byte[i] of the 8-byte value {hi_dw:lo_dw}
+__device__ __forceinline__ uint32_t perm(uint32_t hi_dw, uint32_t lo_dw, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi_dw, lo_dw, sel);
+}
+
+template <int NV>
+struct Sym {
+  uint32_t l[NV];
+  uint32_t h[NV];
+};
+
+// Uniform table view (held in SGPRs after a scalar load).
+struct Tab {
+  uint32_t lo[10];
+  uint32_t hi[10];
+  uint32_t flags;
+};
+
+// `t` must be a wave-uniform address into read-only plan memory. Reading it
+// through the constant address space makes the compiler emit s_load_dwordx*
+// so the table lives in SGPRs (a plain global pointer gives per-lane VMEM loads).
+typedef const __attribute__((address_space(4))) RsTab *ConstTab;
+__device__ __forceinline__ Tab load_tab(const RsTab *t) {
+  ConstTab c = (ConstTab)(t);
+  Tab r;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    r.lo[i] = c->lo[i];
+    r.hi[i] = c->hi[i];
+  }
+  r.flags = c->flags;
+  return r;
+}
+
+// product byte-planes of mul(y) for one dword pair, XORed into (xl, xh)
+__device__ __forceinline__ void mul_acc1(uint32_t &xl, uint32_t &xh, uint32_t yl, uint32_t yh, const Tab &t) {
+  const uint32_t a0 = yl & 0x07070707u, a1 = (yl >> 3) & 0x07070707u, a2 = (yl >> 6) & 0x03030303u;
+  const uint32_t b0 = yh & 0x07070707u, b1 = (yh >> 3) & 0x07070707u, b2 = (yh >> 6) & 0x03030303u;
+  uint32_t l = xor3(xl, perm(t.lo[1], t.lo[0], a0), perm(t.lo[3], t.lo[2], a1));
+  uint32_t h = xor3(xh, perm(t.hi[1], t.hi[0], a0), perm(t.hi[3], t.hi[2], a1));
+  l = xor3(l, perm(t.lo[4], t.lo[4], a2), perm(t.lo[6], t.lo[5], b0));
+  h = xor3(h, perm(t.hi[4], t.hi[4], a2), perm(t.hi[6], t.hi[5], b0));
+  xl = xor3(l, perm(t.lo[8], t.lo[7], b1), perm(t.lo[9], t.lo[9], b2));
+  xh = xor3(h, perm(t.hi[8], t.hi[7], b1), perm(t.hi[9], t.hi[9], b2));
+}
+
+// Generic.zig:234-240 mulAdd: x ^= mul(y)
+template <int NV>
+__device__ __forceinline__ void mul_add(Sym<NV> &x, const Sym<NV> &y, const Tab &t) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) mul_acc1(x.l[v], x.h[v], y.l[v], y.h[v], t);
+}
+
+// Generic.zig:220-231 mulScalar on one register slot: x = mul(x)
+template <int NV>
+__device__ __forceinline__ void mul_inplace(Sym<NV> &x, const Tab &t) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    uint32_t l = 0, h = 0;
+    mul_acc1(l, h, x.l[v], x.h[v], t);
+    x.l[v] = l;
+    x.h[v] = h;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void xor_into(Sym<NV> &a, const Sym<NV> &b) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    a.l[v] ^= b.l[v];
+    a.h[v] ^= b.h[v];
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void zero(Sym<NV> &a) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) a.l[v] = a.h[v] = 0;
+}
+
+// Generic.zig:149-169 fftPartial: x ^= mul(y); y ^= x   (XOR-only: y ^= x)
+template <int NV>
+__device__ __forceinline__ void fft_bf(Sym<NV> &x, Sym<NV> &y, const Tab &t) {
+  if (!(t.flags & kTabXorOnly)) mul_add(x, y, t);
+  xor_into(y, x);
+}
+
+// Generic.zig:171-192 ifftPartial: y ^= x; x ^= mul(y)   (XOR-only: y ^= x)
+template <int NV>
+__device__ __forceinline__ void ifft_bf(Sym<NV> &x, Sym<NV> &y, const Tab &t) {
+  xor_into(y, x);
+  if (!(t.flags & kTabXorOnly)) mul_add(x, y, t);
+}
+
+// ---- register-resident transforms over s[0..SIZE) (pos = 0), compile-time
+// SIZE, run-time truncation. Table order = push_ifft_tabs / push_fft_tabs.
+
+// Generic.zig:80-147
+template <int SIZE, int NV>
+__device__ __forceinline__ void ifft_regs(Sym<NV> *s, const RsTab *__restrict__ tabs, uint32_t trunc) {
+  int ti = 0;
+  int d = 1;
+#pragma unroll
+  for (int d4 = 4; d4 <= SIZE; d4 <<= 2) {
+#pragma unroll
+    for (int r = 0; r < SIZE; r += d4) {
+      if (static_cast<uint32_t>(r) < trunc) {
+        const Tab m01 = load_tab(tabs + ti), m02 = load_tab(tabs + ti + 1), m23 = load_tab(tabs + ti + 2);
+#pragma unroll
+        for (int i = r; i < r + d; i++) {
+          ifft_bf(s[i], s[i + d], m01);
+          ifft_bf(s[i + 2 * d], s[i + 3 * d], m23);
+          ifft_bf(s[i], s[i + 2 * d], m02);
+          ifft_bf(s[i + d], s[i + 3 * d], m02);
+        }
+      }
+      ti += 3;
+    }
+    d = d4;
+  }
+  if (d < SIZE) {  // final odd layer, Generic.zig:131-146
+    const Tab t = load_tab(tabs + ti);
+#pragma unroll
+    for (int i = 0; i < d; i++) ifft_bf(s[i], s[d + i], t);
+  }
+}
+
+// Generic.zig:15-78
+template <int SIZE, int NV>
+__device__ __forceinline__ void fft_regs(Sym<NV> *s, const RsTab *__restrict__ tabs, uint32_t trunc) {
+  int ti = 0;
+  int d4 = SIZE;
+#pragma unroll
+  for (int d = SIZE >> 2; d != 0; d >>= 2) {
+#pragma unroll
+    for (int r = 0; r < SIZE; r += d4) {
+      if (static_cast<uint32_t>(r) < trunc) {
+        const Tab m01 = load_tab(tabs + ti), m02 = load_tab(tabs + ti + 1), m23 = load_tab(tabs + ti + 2);
+#pragma unroll
+        for (int i = r; i < r + d; i++) {
+          fft_bf(s[i], s[i + 2 * d], m02);
+          fft_bf(s[i + d], s[i + 3 * d], m02);
+          fft_bf(s[i], s[i + d], m01);
+          fft_bf(s[i + 2 * d], s[i + 3 * d], m23);
+        }
+      }
+      ti += 3;
+    }
+    d4 = d;
+  }
+  if (d4 == 2) {  // radix-2 tail, Generic.zig:64-77
+#pragma unroll
+    for (int r = 0; r < SIZE; r += 2) {
+      if (static_cast<uint32_t>(r) < trunc) {
+        const Tab t = load_tab(tabs + ti + r / 2);
+        fft_bf(s[r], s[r + 1], t);
+      }
+    }
+  }
+}
+
+// ---- global-memory access for one lane's dword pairs -----------------------
+template <int NV>
+struct VecT;
+template <>
+struct VecT<1> {
+  typedef uint32_t type;
+};
+template <>
+struct VecT<2> {
+  typedef uint32_t __attribute__((ext_vector_type(2))) type;
+};
+template <>
+struct VecT<4> {
+  typedef uint32_t __attribute__((ext_vector_type(4))) type;
+};
+
+template <int NV>
+__device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__ p) {
+  typedef typename VecT<NV>::type V;
+  const V lo = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
+  const V hi = __builtin_nontemporal_load(reinterpret_cast<const V *>(p + 32));
+  if constexpr (NV == 1) {
+    s.l[0] = lo;
+    s.h[0] = hi;
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      s.l[v] = lo[v];
+      s.h[v] = hi[v];
+    }
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void store_sym(uint8_t *__restrict__ p, const Sym<NV> &s) {
+  typedef typename VecT<NV>::type V;
+  V lo, hi;
+  if constexpr (NV == 1) {
+    lo = s.l[0];
+    hi = s.h[0];
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      lo[v] = s.l[v];
+      hi[v] = s.h[v];
+    }
+  }
+  __builtin_nontemporal_store(lo, reinterpret_cast<V *>(p));
+  __builtin_nontemporal_store(hi, reinterpret_cast<V *>(p + 32));
+}
+
+}  // namespace dev
+}  // namespace rs

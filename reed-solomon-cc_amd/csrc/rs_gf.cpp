@@ -1,0 +1,200 @@
+// rs_gf.cpp — field tables, v_perm table builder, FWHT / evalPoly (host).
+// See rs_gf.hpp for the reference citations.
+#include "rs_gf.hpp"
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+
+namespace rs {
+
+namespace {
+
+constexpr uint16_t kCantor[16] = {0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+                                  0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E};
+
+std::unique_ptr<Tables> g_tables;
+std::once_flag g_once;
+
+uint16_t mul16_raw(uint16_t x, uint16_t lm, const uint16_t *exp, const uint16_t *log) {
+  return x == 0 ? 0 : exp[add_mod(log[x], lm)];
+}
+
+void build(Tables &t) {
+  // tables.zig:22-31 — LFSR over the polynomial; `exp` temporarily holds logs.
+  std::memset(&t, 0, sizeof t);
+  uint32_t state = 1;
+  for (uint32_t i = 0; i < kModulus; i++) {
+    t.exp[state] = static_cast<uint16_t>(i);
+    state <<= 1;
+    if (state >= kOrder) state ^= kPolynomial;
+  }
+  t.exp[0] = kModulus;
+  // tables.zig:35-45 — re-express in the Cantor basis, invert.
+  t.log[0] = 0;
+  for (int i = 0; i < 16; i++) {
+    uint32_t w = 1u << i;
+    for (uint32_t j = 0; j < w; j++) t.log[j + w] = t.log[j] ^ kCantor[i];
+  }
+  for (uint32_t i = 0; i < kOrder; i++) t.log[i] = t.exp[t.log[i]];
+  for (uint32_t i = 0; i < kOrder; i++) t.exp[t.log[i]] = static_cast<uint16_t>(i);
+  t.exp[kModulus] = t.exp[0];
+
+  // tables.zig:60-87 — LCH skew factors (as logs).
+  uint16_t temp[15];
+  for (int i = 1; i < 16; i++) temp[i - 1] = static_cast<uint16_t>(1u << i);
+  for (int m = 0; m < 15; m++) {
+    const uint32_t step = 1u << (m + 1);
+    const uint32_t back = (1u << m) - 1;
+    t.skew[back] = 0;
+    for (int i = m; i < 15; i++) {
+      const uint32_t s = 1u << (i + 1);
+      for (uint32_t j = back; j < s; j += step) t.skew[j + s] = t.skew[j] ^ temp[i];
+    }
+    temp[m] = static_cast<uint16_t>(kModulus - t.log[mul16_raw(temp[m], t.log[temp[m] ^ 1], t.exp, t.log)]);
+    for (int i = m + 1; i < 15; i++) temp[i] = mul16_raw(temp[i], add_mod(t.log[temp[i] ^ 1], temp[m]), t.exp, t.log);
+  }
+  for (uint32_t i = 0; i < kModulus; i++) t.skew[i] = t.log[t.skew[i]];
+
+  // tables.zig:146-147
+  std::memcpy(t.log_walsh, t.log, sizeof t.log);
+  fwht(t.log_walsh, kOrder);
+}
+
+}  // namespace
+
+const Tables &tables() {
+  std::call_once(g_once, [] {
+    g_tables.reset(new Tables);
+    build(*g_tables);
+  });
+  return *g_tables;
+}
+
+uint16_t mul16(uint16_t x, uint16_t log_m) {
+  const Tables &t = tables();
+  return mul16_raw(x, log_m, t.exp, t.log);
+}
+
+uint64_t ceil_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+RsTab make_tab(uint16_t log_m, bool quirk_d1) {
+  // field f: bit offset in x and width; tables hold byte_o(mul16(v << off, log_m)).
+  static constexpr int kOff[6] = {0, 3, 6, 8, 11, 14};
+  static constexpr int kBits[6] = {3, 3, 2, 3, 3, 2};
+  static constexpr int kSlot[6] = {0, 2, 4, 5, 7, 9};
+  RsTab t{};
+  for (int f = 0; f < 6; f++) {
+    for (uint32_t v = 0; v < (1u << kBits[f]); v++) {
+      const uint16_t x = static_cast<uint16_t>(v << kOff[f]);
+      // Generic.zig:283 (D1): prod_hi uses t1_hi[lo & 15], i.e. the hi byte of
+      // mul(((lo & 15) << 4) ^ (x & 0xFFF0)) — a different GF(2)-linear map.
+      const uint16_t xh = quirk_d1 ? static_cast<uint16_t>(((x & 0xF) << 4) ^ (x & 0xFFF0)) : x;
+      const uint32_t plo = mul16(x, log_m) & 0xFF;
+      const uint32_t phi = mul16(xh, log_m) >> 8;
+      const int w = kSlot[f] + (v >> 2), sh = 8 * (v & 3);
+      t.lo[w] |= plo << sh;
+      t.hi[w] |= phi << sh;
+    }
+  }
+  t.flags = 0;
+  t.log_m = log_m;
+  return t;
+}
+
+RsTab make_twiddle(uint32_t skew_index, bool quirk_d1) {
+  if (skew_index >= kModulus) {  // beyond the table: only reachable for groups the device skips
+    RsTab z{};
+    z.flags = kTabXorOnly;
+    z.log_m = kModulus;
+    return z;
+  }
+  const uint16_t lm = tables().skew[skew_index];
+  if (lm == kModulus) {
+    RsTab z{};
+    z.flags = kTabXorOnly;
+    z.log_m = kModulus;
+    return z;
+  }
+  return make_tab(lm, quirk_d1);
+}
+
+void fwht(uint16_t *d, uint64_t m) {
+  uint64_t dist = 1, stride = 4;
+  while (stride <= kOrder) {
+    for (uint64_t r = 0; r < m; r += stride) {
+      for (uint64_t o = r; o < r + dist; o++) {
+        // walsh_hadamard.zig:38-62 (fwht4 of two fwht2 layers); offset/stride are u16 there
+        const uint64_t x0 = static_cast<uint16_t>(o), st = static_cast<uint16_t>(dist);
+        const uint64_t x1 = x0 + st, x2 = x0 + 2 * st, x3 = x0 + 3 * st;
+        const uint16_t s0 = add_mod(d[x0], d[x1]), d0 = sub_mod(d[x0], d[x1]);
+        const uint16_t s1 = add_mod(d[x2], d[x3]), d1 = sub_mod(d[x2], d[x3]);
+        d[x0] = add_mod(s0, s1);
+        d[x1] = add_mod(d0, d1);
+        d[x2] = sub_mod(s0, s1);
+        d[x3] = sub_mod(d0, d1);
+      }
+    }
+    dist = stride;
+    stride *= 4;
+  }
+}
+
+void eval_poly(uint16_t *e, uint64_t truncated_size) {
+  const Tables &t = tables();
+  fwht(e, truncated_size);
+  for (uint32_t i = 0; i < kOrder; i++) {
+    const uint32_t p = static_cast<uint32_t>(e[i]) * t.log_walsh[i];
+    e[i] = add_mod(p & 0xFFFF, p >> 16);
+  }
+  fwht(e, kOrder);
+}
+
+size_t ifft_tab_count(uint64_t size) {
+  size_t n = 0;
+  uint64_t d = 1, d4 = 4;
+  for (; d4 <= size; d = d4, d4 <<= 2) n += 3 * (size / d4);
+  if (d < size) n += 1;
+  return n;
+}
+
+size_t fft_tab_count(uint64_t size) {
+  size_t n = 0;
+  uint64_t d = size >> 2, d4 = size;
+  for (; d != 0; d4 = d, d >>= 2) n += 3 * (size / d4);
+  if (d4 == 2) n += size / 2;
+  return n;
+}
+
+void push_ifft_tabs(std::vector<RsTab> &out, uint64_t size, uint64_t sd, bool q) {
+  uint64_t d = 1, d4 = 4;
+  for (; d4 <= size; d = d4, d4 <<= 2) {
+    for (uint64_t r = 0; r < size; r += d4) {
+      const uint64_t base = r + d + sd - 1;  // Generic.zig:88-92
+      out.push_back(make_twiddle(static_cast<uint32_t>(base), q));          // m01
+      out.push_back(make_twiddle(static_cast<uint32_t>(base + d), q));      // m02
+      out.push_back(make_twiddle(static_cast<uint32_t>(base + 2 * d), q));  // m23
+    }
+  }
+  if (d < size) out.push_back(make_twiddle(static_cast<uint32_t>(d + sd - 1), q));  // Generic.zig:131-132
+}
+
+void push_fft_tabs(std::vector<RsTab> &out, uint64_t size, uint64_t sd, bool q) {
+  uint64_t d = size >> 2, d4 = size;
+  for (; d != 0; d4 = d, d >>= 2) {
+    for (uint64_t r = 0; r < size; r += d4) {
+      const uint64_t base = r + d + sd - 1;  // Generic.zig:23-27
+      out.push_back(make_twiddle(static_cast<uint32_t>(base), q));
+      out.push_back(make_twiddle(static_cast<uint32_t>(base + d), q));
+      out.push_back(make_twiddle(static_cast<uint32_t>(base + 2 * d), q));
+    }
+  }
+  if (d4 == 2)  // Generic.zig:64-77
+    for (uint64_t r = 0; r < size; r += 2) out.push_back(make_twiddle(static_cast<uint32_t>(r + sd), q));
+}
+
+}  // namespace rs

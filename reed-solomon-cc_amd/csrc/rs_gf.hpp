@@ -1,0 +1,80 @@
+// rs_gf.hpp — GF(2^16) field tables and the per-multiplier v_perm tables (host side).
+//
+// Field: order 65536, polynomial 0x1002D, 16-element Cantor basis (gf.zig:1-13).
+// Tables are generated once at library load, as tables.zig:22-147 does at build
+// time: exp/log (22-45), LCH skew factors (60-87), log_walsh = FWHT(log) (146-147).
+//
+// Device multiply (rs_device.hpp) works on a GF(2)-linear decomposition of the
+// 16-bit symbol x = lo | hi << 8 into six bit fields — lo[2:0], lo[5:3], lo[7:6],
+// hi[2:0], hi[5:3], hi[7:6] — so each field indexes an <=8-entry byte table that
+// one v_perm_b32 resolves for 4 symbols at once. RsTab holds, for one multiplier
+// exp[log_m], those tables for the low and the high output byte. This replaces
+// the reference's 4 x 16-entry nibble tables (mul_128, tables.zig:96-118) that
+// x86 pshufb needs; both compute mul16(x, log_m) (utilities.zig:5-8) exactly.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace rs {
+
+constexpr uint32_t kOrder = 65536;
+constexpr uint32_t kModulus = 65535;
+constexpr uint32_t kPolynomial = 65581;
+
+// 96-byte table block for one multiplier (uniform across a wave; scalar-loaded).
+// lo[]/hi[]: field tables for the low / high output byte, dword-packed:
+//   [0,1] field lo[2:0] entries 0-3 | 4-7   [2,3] lo[5:3]   [4] lo[7:6]
+//   [5,6] field hi[2:0]                     [7,8] hi[5:3]   [9] hi[7:6]
+struct alignas(16) RsTab {
+  uint32_t lo[10];
+  uint32_t hi[10];
+  uint32_t flags;  // bit 0: twiddle is log 65535 (element 0) -> XOR-only butterfly
+  uint32_t log_m;
+  uint32_t pad[2];
+};
+static_assert(sizeof(RsTab) == 96, "RsTab layout");
+
+constexpr uint32_t kTabXorOnly = 1u;
+
+struct Tables {
+  uint16_t exp[kOrder];
+  uint16_t log[kOrder];
+  uint16_t skew[kModulus];
+  uint16_t log_walsh[kOrder];
+};
+
+const Tables &tables();  // built once, thread-safe
+
+inline uint16_t add_mod(uint32_t x, uint32_t y) {  // utilities.zig:10-13
+  uint32_t s = x + y;
+  return static_cast<uint16_t>(s + (s >> 16));
+}
+inline uint16_t sub_mod(uint32_t x, uint32_t y) {  // utilities.zig:15-18
+  uint32_t d = x + kModulus - y;
+  return static_cast<uint16_t>(d + (d >> 16));
+}
+uint16_t mul16(uint16_t x, uint16_t log_m);  // utilities.zig:5-8
+
+// v_perm tables for multiplication by exp[log_m]; quirk_d1 reproduces
+// Generic.zig:283 (hi product of nibble 0 read from t1_hi).
+RsTab make_tab(uint16_t log_m, bool quirk_d1);
+// Table for an FFT/IFFT twiddle: XOR-only marker when log_m == 65535
+// (the engine's `log_m == gf.modulus` shortcut, Generic.zig:38,47,53,103,...).
+RsTab make_twiddle(uint32_t skew_index, bool quirk_d1);
+
+// walsh_hadamard.zig:16-62 (ones'-complement mod-65535 FWHT, truncated to m)
+void fwht(uint16_t *data, uint64_t m);
+// Generic.zig:200-215
+void eval_poly(uint16_t *erasures, uint64_t truncated_size);
+
+uint64_t ceil_pow2(uint64_t v);
+
+// ---- butterfly schedules: the table sequence a device transform consumes.
+// Mirrors Generic.zig:15-78 (fft) and 80-147 (ifft) group-for-group for ALL
+// groups r < size; the device skips groups r >= truncated_size at run time.
+size_t ifft_tab_count(uint64_t size);
+size_t fft_tab_count(uint64_t size);
+void push_ifft_tabs(std::vector<RsTab> &out, uint64_t size, uint64_t skew_delta, bool quirk_d1);
+void push_fft_tabs(std::vector<RsTab> &out, uint64_t size, uint64_t skew_delta, bool quirk_d1);
+
+}  // namespace rs

@@ -1,0 +1,86 @@
+// rs_internal.hpp — launch interface between the host codec (rs_capi.cpp) and
+// the HIP kernels (rs_kernels.hip). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "rs_gf.hpp"
+
+namespace rs {
+
+// Encode: data [stripe][k][sb] -> parity [stripe][m][sb].
+// Table block: n_chunks x ifft_tab_count(chunk) (chunk j has skew_delta (j+1)*chunk),
+// then fft_tab_count(chunk) (skew_delta 0).
+struct EncodeArgs {
+  const uint8_t *data;
+  uint64_t data_stripe_stride;
+  uint8_t *parity;
+  uint64_t parity_stripe_stride;
+  uint64_t shard_bytes;
+  uint64_t n_stripes;
+  const RsTab *tabs;
+  uint32_t chunk;        // ceilPow2(m)
+  uint32_t n_chunks;     // IFFT chunks actually folded (D2 may drop one)
+  uint32_t trunc_first;  // truncation of chunk 0 = min(k, chunk)
+  uint32_t trunc_last;   // truncation of the last chunk (chunk, or k % chunk)
+  uint32_t m;            // FFT truncation = recovery_count
+  uint32_t k;
+  uint32_t tabs_per_chunk;  // ifft_tab_count(chunk)
+  uint32_t work;            // Wenc = alignUp(k, chunk) (generic path scratch positions)
+  uint8_t *scratch;      // generic path only: [stripe][Wenc][sb]
+  uint64_t scratch_stripes;
+};
+
+// Reconstruct: positions per root.zig:199-229 (recovery at [0,m), originals at
+// [chunk, chunk+k), W = ceilPow2(chunk+k)). Plan arrays (device, uniform):
+//   pos_src[W]: -1 none, else shard index | kSrcRecovery for recovery shards
+//   pos_dst[W]: -1, else the restored slot of a missing original
+//   tab_pre[W]: multiply by exp[erasures[p]] (present positions)
+//   tab_post[W]: multiply by exp[65535 - erasures[p]] (missing originals)
+struct DecodeArgs {
+  const uint8_t *orig;
+  uint64_t orig_stripe_stride;
+  const uint8_t *rec;
+  uint64_t rec_stripe_stride;
+  uint8_t *out;
+  uint64_t out_stripe_stride;
+  uint64_t shard_bytes;
+  uint64_t n_stripes;
+  const RsTab *tab_ifft;
+  const RsTab *tab_fft;
+  const RsTab *tab_pre;
+  const RsTab *tab_post;
+  const int32_t *pos_src;
+  const int32_t *pos_dst;
+  uint32_t work;   // W
+  uint32_t trunc;  // chunk + k
+  uint8_t *scratch;  // generic path only: [stripe][W][sb]
+  uint64_t scratch_stripes;
+};
+constexpr int32_t kSrcRecovery = 0x40000000;
+constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
+
+// Kernel variants: fused register-resident for small transforms, generic
+// (per-lane column walk over an HBM scratch work buffer) otherwise.
+enum class Variant { kRegister, kGeneric };
+
+struct KernelChoice {
+  Variant variant;
+  int size;  // chunk (encode) or W (decode) for register kernels
+  int nv;    // dword pairs per lane
+  const char *name;
+};
+
+// max_nv: widest per-lane access (1, 2, 4 dword pairs) the pointer/stride alignment allows
+KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
+KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
+
+hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
+hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s);
+
+// Engine shims (generic, in place on a single-stripe work buffer)
+hipError_t launch_engine_fft(uint8_t *work, uint64_t shard_bytes, uint64_t pos, uint64_t size, uint64_t trunc,
+                             const RsTab *tabs, bool inverse, hipStream_t s);
+hipError_t launch_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab, hipStream_t s);
+
+}  // namespace rs

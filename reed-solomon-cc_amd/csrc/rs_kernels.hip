@@ -1,0 +1,480 @@
+// rs_kernels.hip — HIP kernels for gfx950 (MI355X): Reed-Solomon encode and
+// reconstruct over GF(2^16) with the additive FFT of usebeforefree/reed-solomon-cc.
+//
+// Parallelisation: every 64-byte chunk column of a stripe is an
+// independent code, so a lane owns NV dword pairs (4*NV symbols) of one column
+// and runs the WHOLE codec for it — no cross-lane exchange, no barriers, no LDS.
+// Grid: x = column units of one stripe (256 lanes per block), y = stripes.
+//
+//  * k_encode_reg<C, NV>: fused encode, the chunk-sized transforms in VGPRs.
+//    HBM traffic = k shards read + m shards written per stripe (the minimum).
+//    Mirrors Encoder.encode (root.zig:136-173).
+//  * k_decode_reg<W, NV>: fused reconstruct, the W-point transforms in VGPRs.
+//    Reads the k+m-e received shards it needs, writes the e restored ones.
+//    Mirrors Decoder.decode (root.zig:268-335).
+//  * k_encode_generic / k_decode_generic: the same codec for any (k, m), each
+//    lane walking its column through a global scratch work buffer
+//    [stripe][W][shard_bytes] (the reference's Shards layout, root.zig:350-395).
+//  * k_engine_transform / k_mul_scalar: the Engine seam (Generic.zig) as test shims.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "rs_device.hpp"
+#include "rs_internal.hpp"
+
+namespace rs {
+namespace {
+
+using dev::Sym;
+using dev::Tab;
+
+constexpr int kBlock = 256;
+
+__host__ __device__ constexpr int ifft_tabs_ce(int size) {
+  int n = 0, d = 1, d4 = 4;
+  for (; d4 <= size; d = d4, d4 <<= 2) n += 3 * (size / d4);
+  return n + (d < size ? 1 : 0);
+}
+
+// byte offset of this lane's dword pairs inside a shard; false if out of range
+template <int NV>
+__device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, uint64_t &off) {
+  constexpr uint32_t kUnitsPerChunk = 8 / NV;
+  const uint64_t unit = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t units = shard_bytes / 64 * kUnitsPerChunk;
+  if (unit >= units) return false;
+  off = unit / kUnitsPerChunk * 64 + unit % kUnitsPerChunk * (4 * NV);
+  return true;
+}
+
+// ============================================================ fused encode
+template <int C, int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
+  uint64_t off;
+  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  constexpr int TI = ifft_tabs_ce(C);
+  const uint64_t sb = a.shard_bytes;
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *src = a.data + s * a.data_stripe_stride + off;
+    Sym<NV> acc[C];
+    // first chunk: root.zig:143-146
+#pragma unroll
+    for (int p = 0; p < C; p++) {
+      if (static_cast<uint32_t>(p) < a.trunc_first) dev::load_sym(acc[p], src + p * sb);
+      else dev::zero(acc[p]);
+    }
+    dev::ifft_regs<C>(acc, a.tabs, a.trunc_first);
+    // further chunks, IFFT + XOR-fold: root.zig:148-167
+    for (uint32_t j = 1; j < a.n_chunks; j++) {
+      const uint32_t t = (j + 1 == a.n_chunks) ? a.trunc_last : static_cast<uint32_t>(C);
+      const uint8_t *cs = src + static_cast<uint64_t>(j) * C * sb;
+      Sym<NV> cur[C];
+#pragma unroll
+      for (int p = 0; p < C; p++) {
+        if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb);
+        else dev::zero(cur[p]);
+      }
+      dev::ifft_regs<C>(cur, a.tabs + j * TI, t);
+#pragma unroll
+      for (int p = 0; p < C; p++) dev::xor_into(acc[p], cur[p]);
+    }
+    // root.zig:169
+    dev::fft_regs<C>(acc, a.tabs + a.n_chunks * TI, a.m);
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
+#pragma unroll
+    for (int p = 0; p < C; p++)
+      if (static_cast<uint32_t>(p) < a.m) dev::store_sym(dst + p * sb, acc[p]);
+  }
+}
+
+// ======================================================= fused reconstruct
+// root.zig:309-315 formal derivative over W register slots
+template <int W, int NV>
+__device__ __forceinline__ void derivative_regs(Sym<NV> *w) {
+#pragma unroll
+  for (int i = 1; i < W; i++) {
+    const int width = i & -i;
+#pragma unroll
+    for (int j = 0; j < width; j++) dev::xor_into(w[i - width + j], w[i + j]);
+  }
+}
+
+template <int W, int NV>
+__global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
+  uint64_t off;
+  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  const uint64_t sb = a.shard_bytes;
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
+    const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+    Sym<NV> w[W];
+    // erasure masks on received shards, zero elsewhere: root.zig:291-303
+#pragma unroll
+    for (int p = 0; p < W; p++) {
+      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)a.pos_src)[p];
+      if (src >= 0) {
+        const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
+        dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
+        dev::mul_inplace(w[p], dev::load_tab(a.tab_pre + p));
+      } else {
+        dev::zero(w[p]);
+      }
+    }
+    dev::ifft_regs<W>(w, a.tab_ifft, a.trunc);  // root.zig:306
+    derivative_regs<W>(w);                      // root.zig:309-315
+    dev::fft_regs<W>(w, a.tab_fft, a.trunc);    // root.zig:318
+    uint8_t *out = a.out + s * a.out_stripe_stride + off;
+#pragma unroll
+    for (int p = 0; p < W; p++) {  // root.zig:321-326
+      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)a.pos_dst)[p];
+      if (dst >= 0) {
+        dev::mul_inplace(w[p], dev::load_tab(a.tab_post + p));
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, w[p]);
+      }
+    }
+  }
+}
+
+// ============================================ generic: column walk in HBM scratch
+template <int NV>
+__device__ __forceinline__ void ld(Sym<NV> &s, const uint8_t *p) {
+  typedef typename dev::VecT<NV>::type V;
+  const V lo = *reinterpret_cast<const V *>(p), hi = *reinterpret_cast<const V *>(p + 32);
+  if constexpr (NV == 1) {
+    s.l[0] = lo;
+    s.h[0] = hi;
+  } else {
+    for (int v = 0; v < NV; v++) {
+      s.l[v] = lo[v];
+      s.h[v] = hi[v];
+    }
+  }
+}
+template <int NV>
+__device__ __forceinline__ void st(uint8_t *p, const Sym<NV> &s) {
+  typedef typename dev::VecT<NV>::type V;
+  V lo, hi;
+  if constexpr (NV == 1) {
+    lo = s.l[0];
+    hi = s.h[0];
+  } else {
+    for (int v = 0; v < NV; v++) {
+      lo[v] = s.l[v];
+      hi[v] = s.h[v];
+    }
+  }
+  *reinterpret_cast<V *>(p) = lo;
+  *reinterpret_cast<V *>(p + 32) = hi;
+}
+
+// Generic.zig:80-147 on positions base + p*ps (runtime size / truncation)
+template <int NV>
+__device__ void ifft_mem(uint8_t *w, uint64_t ps, uint64_t pos, uint64_t size, uint64_t trunc,
+                         const RsTab *__restrict__ tabs) {
+  uint64_t ti = 0, d = 1;
+  for (uint64_t d4 = 4; d4 <= size; d = d4, d4 <<= 2) {
+    const uint64_t rmax = trunc < size ? trunc : size;
+    for (uint64_t r = 0; r < rmax; r += d4) {
+      const RsTab *g = tabs + ti + 3 * (r / d4);
+      const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+      for (uint64_t i = r; i < r + d; i++) {
+        uint8_t *p0 = w + (pos + i) * ps, *p1 = p0 + d * ps, *p2 = p1 + d * ps, *p3 = p2 + d * ps;
+        Sym<NV> s0, s1, s2, s3;
+        ld(s0, p0);
+        ld(s1, p1);
+        ld(s2, p2);
+        ld(s3, p3);
+        dev::ifft_bf(s0, s1, m01);
+        dev::ifft_bf(s2, s3, m23);
+        dev::ifft_bf(s0, s2, m02);
+        dev::ifft_bf(s1, s3, m02);
+        st(p0, s0);
+        st(p1, s1);
+        st(p2, s2);
+        st(p3, s3);
+      }
+    }
+    ti += 3 * (size / d4);
+  }
+  if (d < size) {
+    const Tab t = dev::load_tab(tabs + ti);
+    for (uint64_t i = 0; i < d; i++) {
+      uint8_t *p0 = w + (pos + i) * ps, *p1 = w + (pos + d + i) * ps;
+      Sym<NV> s0, s1;
+      ld(s0, p0);
+      ld(s1, p1);
+      dev::ifft_bf(s0, s1, t);
+      st(p0, s0);
+      st(p1, s1);
+    }
+  }
+}
+
+// Generic.zig:15-78
+template <int NV>
+__device__ void fft_mem(uint8_t *w, uint64_t ps, uint64_t pos, uint64_t size, uint64_t trunc,
+                        const RsTab *__restrict__ tabs) {
+  uint64_t ti = 0, d4 = size;
+  for (uint64_t d = size >> 2; d != 0; d4 = d, d >>= 2) {
+    const uint64_t rmax = trunc < size ? trunc : size;
+    for (uint64_t r = 0; r < rmax; r += d4) {
+      const RsTab *g = tabs + ti + 3 * (r / d4);
+      const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+      for (uint64_t i = r; i < r + d; i++) {
+        uint8_t *p0 = w + (pos + i) * ps, *p1 = p0 + d * ps, *p2 = p1 + d * ps, *p3 = p2 + d * ps;
+        Sym<NV> s0, s1, s2, s3;
+        ld(s0, p0);
+        ld(s1, p1);
+        ld(s2, p2);
+        ld(s3, p3);
+        dev::fft_bf(s0, s2, m02);
+        dev::fft_bf(s1, s3, m02);
+        dev::fft_bf(s0, s1, m01);
+        dev::fft_bf(s2, s3, m23);
+        st(p0, s0);
+        st(p1, s1);
+        st(p2, s2);
+        st(p3, s3);
+      }
+    }
+    ti += 3 * (size / d4);
+  }
+  if (d4 == 2) {
+    for (uint64_t r = 0; r < trunc; r += 2) {
+      const Tab t = dev::load_tab(tabs + ti + r / 2);
+      uint8_t *p0 = w + (pos + r) * ps, *p1 = p0 + ps;
+      Sym<NV> s0, s1;
+      ld(s0, p0);
+      ld(s1, p1);
+      dev::fft_bf(s0, s1, t);
+      st(p0, s0);
+      st(p1, s1);
+    }
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void xor_mem(uint8_t *a, const uint8_t *b) {
+  Sym<NV> x, y;
+  ld(x, a);
+  ld(y, b);
+  dev::xor_into(x, y);
+  st(a, x);
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
+  uint64_t off;
+  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  const uint64_t sb = a.shard_bytes, C = a.chunk;
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *src = a.data + s * a.data_stripe_stride + off;
+    uint8_t *work = a.scratch + s * a.work * sb + off;
+    for (uint32_t j = 0; j < a.n_chunks; j++) {
+      const uint64_t t = j == 0 ? a.trunc_first : (j + 1 == a.n_chunks ? a.trunc_last : C);
+      for (uint64_t p = 0; p < C; p++) {
+        Sym<NV> v;
+        if (p < t) ld(v, src + (j * C + p) * sb);
+        else dev::zero(v);
+        st(work + (j * C + p) * sb, v);
+      }
+      ifft_mem<NV>(work, sb, j * C, C, t, a.tabs + static_cast<uint64_t>(j) * a.tabs_per_chunk);
+      if (j > 0)
+        for (uint64_t p = 0; p < C; p++) xor_mem<NV>(work + p * sb, work + (j * C + p) * sb);
+    }
+    fft_mem<NV>(work, sb, 0, C, a.m, a.tabs + static_cast<uint64_t>(a.n_chunks) * a.tabs_per_chunk);
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
+    for (uint64_t p = 0; p < a.m; p++) {
+      Sym<NV> v;
+      ld(v, work + p * sb);
+      dev::store_sym(dst + p * sb, v);
+    }
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
+  uint64_t off;
+  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  const uint64_t sb = a.shard_bytes, W = a.work;
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
+    const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+    uint8_t *work = a.scratch + s * W * sb + off;
+    for (uint64_t p = 0; p < W; p++) {
+      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)a.pos_src)[p];
+      Sym<NV> v;
+      if (src >= 0) {
+        const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
+        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
+        dev::mul_inplace(v, dev::load_tab(a.tab_pre + p));
+      } else {
+        dev::zero(v);
+      }
+      st(work + p * sb, v);
+    }
+    ifft_mem<NV>(work, sb, 0, W, a.trunc, a.tab_ifft);
+    for (uint64_t i = 1; i < W; i++) {
+      const uint64_t width = i & (~i + 1);
+      for (uint64_t j = 0; j < width; j++) xor_mem<NV>(work + (i - width + j) * sb, work + (i + j) * sb);
+    }
+    fft_mem<NV>(work, sb, 0, W, a.trunc, a.tab_fft);
+    uint8_t *out = a.out + s * a.out_stripe_stride + off;
+    for (uint64_t p = 0; p < W; p++) {
+      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)a.pos_dst)[p];
+      if (dst >= 0) {
+        Sym<NV> v;
+        ld(v, work + p * sb);
+        dev::mul_inplace(v, dev::load_tab(a.tab_post + p));
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, v);
+      }
+    }
+  }
+}
+
+// ========================================================== engine test shims
+__global__ __launch_bounds__(kBlock) void k_engine_transform(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size,
+                                                             uint64_t trunc, const RsTab *tabs, int inverse) {
+  uint64_t off;
+  if (!lane_offset<1>(sb, off)) return;
+  if (inverse) ifft_mem<1>(work + off, sb, pos, size, trunc, tabs);
+  else fft_mem<1>(work + off, sb, pos, size, trunc, tabs);
+}
+
+__global__ __launch_bounds__(kBlock) void k_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab) {
+  uint64_t off;
+  if (!lane_offset<1>(bytes, off)) return;
+  Sym<1> v;
+  ld(v, chunks + off);
+  dev::mul_inplace(v, dev::load_tab(tab));
+  st(chunks + off, v);
+}
+
+dim3 grid_for(uint64_t shard_bytes, int nv, uint64_t n_stripes) {
+  const uint64_t units = shard_bytes / 64 * (8 / nv);
+  const uint64_t bx = (units + kBlock - 1) / kBlock;
+  const uint64_t by = n_stripes < 65535 ? n_stripes : 65535;
+  return dim3(static_cast<uint32_t>(bx), static_cast<uint32_t>(by ? by : 1), 1);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- selection
+// Instantiated register variants: (size, NV) with size*2*NV VGPRs of live state
+// kept <= 128 per lane for encode (acc + one chunk) and decode (W slots).
+static int clamp_nv(int nv, int size, bool enc) {
+  const int live = enc ? 2 * size : size;  // symbol slots live at once
+  while (nv > 1 && live * 2 * nv > 128) nv >>= 1;
+  return nv;
+}
+
+static int env_nv(int dflt) {
+  const char *e = getenv("RS_AMD_NV");
+  if (!e) return dflt;
+  const int v = atoi(e);
+  return (v == 1 || v == 2 || v == 4) ? v : dflt;
+}
+
+static const char *reg_name(bool enc, int size, int nv) {
+  static const char *kEnc[6][3] = {
+      {"encode_reg_w1_nv1", "encode_reg_w1_nv2", "encode_reg_w1_nv4"},
+      {"encode_reg_w2_nv1", "encode_reg_w2_nv2", "encode_reg_w2_nv4"},
+      {"encode_reg_w4_nv1", "encode_reg_w4_nv2", "encode_reg_w4_nv4"},
+      {"encode_reg_w8_nv1", "encode_reg_w8_nv2", "encode_reg_w8_nv4"},
+      {"encode_reg_w16_nv1", "encode_reg_w16_nv2", "encode_reg_w16_nv4"},
+      {"encode_reg_w32_nv1", "encode_reg_w32_nv2", "encode_reg_w32_nv4"}};
+  static const char *kDec[6][3] = {
+      {"decode_reg_w1_nv1", "decode_reg_w1_nv2", "decode_reg_w1_nv4"},
+      {"decode_reg_w2_nv1", "decode_reg_w2_nv2", "decode_reg_w2_nv4"},
+      {"decode_reg_w4_nv1", "decode_reg_w4_nv2", "decode_reg_w4_nv4"},
+      {"decode_reg_w8_nv1", "decode_reg_w8_nv2", "decode_reg_w8_nv4"},
+      {"decode_reg_w16_nv1", "decode_reg_w16_nv2", "decode_reg_w16_nv4"},
+      {"decode_reg_w32_nv1", "decode_reg_w32_nv2", "decode_reg_w32_nv4"}};
+  int si = 0;
+  while ((1 << si) < size) si++;
+  const int ni = nv == 1 ? 0 : nv == 2 ? 1 : 2;
+  return enc ? kEnc[si][ni] : kDec[si][ni];
+}
+
+KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
+  (void)k;
+  (void)shard_bytes;
+  const uint64_t C = ceil_pow2(m);
+  if (C <= 16) {
+    const int c = static_cast<int>(C);
+    const int nv = clamp_nv(std::min(env_nv(4), max_nv), c, true);
+    return {Variant::kRegister, c, nv, reg_name(true, c, nv)};
+  }
+  return {Variant::kGeneric, static_cast<int>(C), 1, "encode_generic_nv1"};
+}
+
+KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
+  (void)shard_bytes;
+  const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
+  if (W <= 32) {
+    const int w = static_cast<int>(W);
+    const int nv = clamp_nv(std::min(env_nv(4), max_nv), w, false);
+    return {Variant::kRegister, w, nv, reg_name(false, w, nv)};
+  }
+  return {Variant::kGeneric, static_cast<int>(W), 1, "decode_generic_nv1"};
+}
+
+#define RS_ENC_CASE(C_, NV_)                                                  \
+  if (kc.size == C_ && kc.nv == NV_) {                                        \
+    hipLaunchKernelGGL((k_encode_reg<C_, NV_>), grid, dim3(kBlock), 0, s, a); \
+    return hipGetLastError();                                                 \
+  }
+#define RS_DEC_CASE(W_, NV_)                                                  \
+  if (kc.size == W_ && kc.nv == NV_) {                                        \
+    hipLaunchKernelGGL((k_decode_reg<W_, NV_>), grid, dim3(kBlock), 0, s, a); \
+    return hipGetLastError();                                                 \
+  }
+
+hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
+  const dim3 grid = grid_for(a.shard_bytes, kc.nv, a.n_stripes);
+  if (kc.variant == Variant::kRegister) {
+    // live slots 2*C: NV <= 128 / (4*C)
+    RS_ENC_CASE(1, 1) RS_ENC_CASE(1, 2) RS_ENC_CASE(1, 4)
+    RS_ENC_CASE(2, 1) RS_ENC_CASE(2, 2) RS_ENC_CASE(2, 4)
+    RS_ENC_CASE(4, 1) RS_ENC_CASE(4, 2) RS_ENC_CASE(4, 4)
+    RS_ENC_CASE(8, 1) RS_ENC_CASE(8, 2)
+    RS_ENC_CASE(16, 1)
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(k_encode_generic<1>, grid, dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
+  const dim3 grid = grid_for(a.shard_bytes, kc.nv, a.n_stripes);
+  if (kc.variant == Variant::kRegister) {
+    // live slots W: NV <= 128 / (2*W)
+    RS_DEC_CASE(2, 1) RS_DEC_CASE(2, 2) RS_DEC_CASE(2, 4)
+    RS_DEC_CASE(4, 1) RS_DEC_CASE(4, 2) RS_DEC_CASE(4, 4)
+    RS_DEC_CASE(8, 1) RS_DEC_CASE(8, 2) RS_DEC_CASE(8, 4)
+    RS_DEC_CASE(16, 1) RS_DEC_CASE(16, 2) RS_DEC_CASE(16, 4)
+    RS_DEC_CASE(32, 1) RS_DEC_CASE(32, 2)
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(k_decode_generic<1>, grid, dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_engine_fft(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
+                             const RsTab *tabs, bool inverse, hipStream_t s) {
+  const dim3 grid = grid_for(sb, 1, 1);
+  hipLaunchKernelGGL(k_engine_transform, grid, dim3(kBlock), 0, s, work, sb, pos, size, trunc, tabs,
+                     inverse ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab, hipStream_t s) {
+  const dim3 grid = grid_for(bytes, 1, 1);
+  hipLaunchKernelGGL(k_mul_scalar, grid, dim3(kBlock), 0, s, chunks, bytes, tab);
+  return hipGetLastError();
+}
+
+}  // namespace rs

@@ -1,0 +1,282 @@
+"""reedsol_amd — Python mirror of the usebeforefree/reed-solomon-cc codec API.
+
+Same names, argument meaning and error behaviour as the reference's module
+``reedsol`` (src/root.zig): ``encode``, ``decode``, ``Encoder``, ``Decoder``,
+``use_high_rate``; errors are raised as ``ReedSolomonError`` subclasses named
+after the Zig error set. Everything is computed by the gfx950 HIP kernels of
+``librs_amd.so`` through its C ABI (include/reedsol.h); there is no CPU
+fallback — without the library or a gfx950 device every call raises.
+
+Device batch API (``encode_batch_dev`` / ``reconstruct_batch_dev``) takes
+torch tensors that already live in HBM (PyTorch is only the allocator and
+stream provider here).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RS_AMD_LIB", os.path.join(PKG_DIR, "build", "librs_amd.so"))
+
+FLAG_CORRECTED = 0
+FLAG_QUIRK_D1 = 1
+FLAG_QUIRK_D2 = 2
+FLAG_REF_LITERAL = 3
+
+_STATUS_NAMES = [
+    "Ok", "TooFewOriginalShards", "NotEnoughShards", "InvalidShardSize", "UnsupportedShardCount",
+    "TooManyOriginalShards", "DifferentShardSize", "InvalidShardIndex", "DuplicateShardIndex",
+    "TooManyShards", "OutOfMemory", "Overflow", "LowRateUnsupported", "ShardTailUnsupported",
+    "InvalidArgument", "DeviceError", "NoDevice",
+]
+
+
+class ReedSolomonError(Exception):
+    status = -1
+
+
+_ERRORS = {}
+for _i, _n in enumerate(_STATUS_NAMES[1:], start=1):
+    _cls = type(_n, (ReedSolomonError,), {"status": _i})
+    globals()[_n] = _cls
+    _ERRORS[_i] = _cls
+
+_lib = None
+
+
+def lib():
+    """Load librs_amd.so (import torch first when mixing with torch tensors so
+    both share one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"librs_amd.so not built: {LIB_PATH} (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, u8p, u16p, sz, u64, u32 = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint16), C.c_size_t, \
+        C.c_uint64, C.c_uint32
+    pp = C.POINTER(C.c_void_p)
+    sig = {
+        "rs_version": (C.c_char_p, []),
+        "rs_status_name": (C.c_char_p, [C.c_int]),
+        "rs_last_error": (C.c_char_p, []),
+        "rs_use_high_rate": (C.c_int, [u64, u64]),
+        "rs_encode": (C.c_int, [u64, u64, sz, pp, pp]),
+        "rs_decode": (C.c_int, [u64, u64, sz, pp, pp, pp]),
+        "rs_encoder_new": (C.c_int, [u64, u64, sz, C.POINTER(vp)]),
+        "rs_encoder_add_original_shard": (C.c_int, [vp, vp, sz]),
+        "rs_encoder_encode": (C.c_int, [vp, pp]),
+        "rs_encoder_reset": (C.c_int, [vp]),
+        "rs_encoder_free": (None, [vp]),
+        "rs_decoder_new": (C.c_int, [u64, u64, sz, C.POINTER(vp)]),
+        "rs_decoder_add_original_shard": (C.c_int, [vp, u64, vp, sz]),
+        "rs_decoder_add_recovery_shard": (C.c_int, [vp, u64, vp, sz]),
+        "rs_decoder_decode": (C.c_int, [vp, pp]),
+        "rs_decoder_free": (None, [vp]),
+        "rs_encode_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32, vp]),
+        "rs_reconstruct_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32, vp]),
+        "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
+        "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz]),
+        "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
+        "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
+        "rs_engine_mul_scalar": (C.c_int, [vp, sz, C.c_uint16, u32]),
+        "rs_engine_eval_poly": (C.c_int, [vp, u64]),
+        "rs_table_exp": (u16p, []),
+        "rs_table_log": (u16p, []),
+        "rs_table_skew": (u16p, []),
+        "rs_table_log_walsh": (u16p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(status: int):
+    if status:
+        detail = lib().rs_last_error().decode(errors="replace")
+        raise _ERRORS.get(status, ReedSolomonError)(detail)
+
+
+def _buf(b) -> C.Array:
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        return (C.c_uint8 * len(b)).from_buffer_copy(bytes(b))
+    import numpy as np
+    a = np.ascontiguousarray(b, dtype=np.uint8)
+    return (C.c_uint8 * a.size).from_buffer_copy(a.tobytes())
+
+
+def use_high_rate(original_count: int, recovery_count: int) -> bool:
+    """root.zig:397-415."""
+    r = lib().rs_use_high_rate(original_count, recovery_count)
+    if r < 0:
+        _check(-r)
+    return bool(r)
+
+
+def encode(original_count: int, recovery_count: int, original: Sequence[bytes]) -> list:
+    """root.zig:14-30 (Encoder.init -> addOriginalShard x n -> encode): the recovery shards."""
+    if len(original) == 0:
+        raise TooFewOriginalShards("no original shards")  # noqa: F821 (generated class), root.zig:20
+    enc = Encoder(original_count, recovery_count, len(original[0]))
+    try:
+        for o in original:
+            enc.add_original_shard(o)
+        return enc.encode()
+    finally:
+        enc.deinit()
+
+
+def decode(original_count: int, recovery_count: int, original: Sequence[Optional[bytes]],
+           recovery: Sequence[Optional[bytes]]) -> list:
+    """root.zig:32-84: all original shards (present ones copied through)."""
+    sb = next((len(r) for r in recovery[:recovery_count] if r is not None), None)
+    if sb is None:  # root.zig:42-58
+        if all(original[i] is not None for i in range(original_count)):
+            return [bytes(original[i]) for i in range(original_count)]
+        raise NotEnoughShards("no recovery shards and originals incomplete")  # noqa: F821
+    dec = Decoder(original_count, recovery_count, sb)
+    try:
+        for i in range(original_count):
+            if original[i] is not None:
+                dec.add_original_shard(i, original[i])
+        for i in range(recovery_count):
+            if recovery[i] is not None:
+                dec.add_recovery_shard(i, recovery[i])
+        return dec.decode()
+    finally:
+        dec.deinit()
+
+
+class Encoder:
+    """root.zig:86-174 Encoder{init, addOriginalShard, encode, deinit}."""
+
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int):
+        self._h = C.c_void_p()
+        _check(lib().rs_encoder_new(original_count, recovery_count, shard_bytes, C.byref(self._h)))
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    def add_original_shard(self, shard: bytes):
+        b = _buf(shard)
+        _check(lib().rs_encoder_add_original_shard(self._h, C.addressof(b), len(shard)))
+
+    def encode(self) -> list:
+        out = (C.c_void_p * self.recovery_count)()
+        _check(lib().rs_encoder_encode(self._h, out))
+        return [C.string_at(p, self.shard_bytes) for p in out]
+
+    def reset(self):
+        _check(lib().rs_encoder_reset(self._h))
+
+    def deinit(self):
+        if self._h:
+            lib().rs_encoder_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.deinit()
+        except Exception:
+            pass
+
+
+class Decoder:
+    """root.zig:176-336 Decoder (private in the reference; same checks)."""
+
+    def __init__(self, original_count: int, recovery_count: int, shard_bytes: int):
+        self._h = C.c_void_p()
+        _check(lib().rs_decoder_new(original_count, recovery_count, shard_bytes, C.byref(self._h)))
+        self.original_count, self.recovery_count, self.shard_bytes = original_count, recovery_count, shard_bytes
+
+    def add_original_shard(self, index: int, shard: bytes):
+        b = _buf(shard)
+        _check(lib().rs_decoder_add_original_shard(self._h, index, C.addressof(b), len(shard)))
+
+    def add_recovery_shard(self, index: int, shard: bytes):
+        b = _buf(shard)
+        _check(lib().rs_decoder_add_recovery_shard(self._h, index, C.addressof(b), len(shard)))
+
+    def decode(self) -> list:
+        out = (C.c_void_p * self.original_count)()
+        _check(lib().rs_decoder_decode(self._h, out))
+        return [C.string_at(p, self.shard_bytes) for p in out]
+
+    def deinit(self):
+        if self._h:
+            lib().rs_decoder_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.deinit()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------ device batch API
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+def encode_batch_dev(original_count: int, recovery_count: int, data, parity, flags: int = FLAG_CORRECTED,
+                     stream=None):
+    """data: uint8 CUDA tensor [n, k, shard_bytes] -> parity [n, m, shard_bytes] (in place).
+
+    Asynchronous on `stream` (default: torch's current stream)."""
+    n, k, sb = data.shape
+    assert k == original_count and parity.shape == (n, recovery_count, sb)
+    assert data.is_cuda and parity.is_cuda and data.is_contiguous() and parity.is_contiguous()
+    _check(lib().rs_encode_batch_dev(original_count, recovery_count, sb, n, C.c_void_p(data.data_ptr()), 0,
+                                     C.c_void_p(parity.data_ptr()), 0, flags, _stream_handle(stream)))
+
+
+def reconstruct_batch_dev(original_count: int, recovery_count: int, present: Sequence[bool], original,
+                          recovery, restored, flags: int = FLAG_CORRECTED, stream=None):
+    """original [n, k, sb], recovery [n, m, sb] (missing slots unread) -> restored [n, e, sb]."""
+    n, k, sb = original.shape
+    pres = (C.c_uint8 * (original_count + recovery_count))(*[1 if p else 0 for p in present])
+    _check(lib().rs_reconstruct_batch_dev(
+        original_count, recovery_count, sb, n, pres, C.c_void_p(original.data_ptr()), original.stride(0),
+        C.c_void_p(recovery.data_ptr()), recovery.stride(0), C.c_void_p(restored.data_ptr()), restored.stride(0),
+        flags, _stream_handle(stream)))
+
+
+def encode_kernel_name(k, m, shard_bytes) -> str:
+    return lib().rs_encode_kernel_name(k, m, shard_bytes).decode()
+
+
+def reconstruct_kernel_name(k, m, shard_bytes) -> str:
+    return lib().rs_reconstruct_kernel_name(k, m, shard_bytes).decode()
+
+
+# ------------------------------------------------------------ engine test shims
+def engine_fft(shards: bytearray, shard_count, shard_bytes, pos, size, trunc, skew_delta, flags=0, inverse=False):
+    buf = (C.c_uint8 * len(shards)).from_buffer(shards)
+    f = lib().rs_engine_ifft if inverse else lib().rs_engine_fft
+    _check(f(C.addressof(buf), shard_count, shard_bytes, pos, size, trunc, skew_delta, flags))
+
+
+def engine_mul_scalar(chunks: bytearray, log_m: int, flags=0):
+    buf = (C.c_uint8 * len(chunks)).from_buffer(chunks)
+    _check(lib().rs_engine_mul_scalar(C.addressof(buf), len(chunks), log_m, flags))
+
+
+def engine_eval_poly(erasures, truncated_size: int):
+    """erasures: numpy uint16[65536], in place (host FWHT, Generic.zig:200-215)."""
+    _check(lib().rs_engine_eval_poly(erasures.ctypes.data_as(C.c_void_p), truncated_size))
+
+
+def table(name: str):
+    import numpy as np
+    n = {"exp": 65536, "log": 65536, "skew": 65535, "log_walsh": 65536}[name]
+    p = getattr(lib(), "rs_table_" + name)()
+    return np.ctypeslib.as_array(p, shape=(n,)).copy()

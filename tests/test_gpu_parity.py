@@ -1,0 +1,250 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle and
+the reference's golden vectors. Bit-exact everywhere (integer/byte work).
+
+Sizes: the oracle runs every small case in full; at BASELINE sizes
+(RS(10,4) 1 MiB, RS(200,55) 256 KiB) parity is checked by size-independent
+properties — encode -> erase -> reconstruct round trips — plus oracle
+comparison on randomly sampled 64-byte columns (column independence,
+SURVEY.md §A.6, itself pinned by tests/test_oracle_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import digest, iota_input, load, splitmix_bytes, survey_input
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from rs_amd import reedsol_amd as R  # noqa: E402  (after torch: share its HIP runtime)
+
+DEV = torch.device("cuda:0")
+
+
+def to_dev(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def gpu_encode(k, m, data: np.ndarray, flags=0):
+    """data [n, k, sb] -> parity [n, m, sb] through rs_encode_batch_dev."""
+    d = to_dev(data)
+    p = torch.zeros((data.shape[0], m, data.shape[2]), dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p, flags)
+    torch.cuda.synchronize()
+    return p.cpu().numpy()
+
+
+def gpu_reconstruct(k, m, present, data: np.ndarray, parity: np.ndarray, flags=0):
+    n, _, sb = data.shape
+    e = int(k - np.sum(present[:k]))
+    o = to_dev(data)
+    r = to_dev(parity)
+    out = torch.zeros((n, max(e, 1), sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, o, r, out, flags)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()[:, :e]
+
+
+@pytest.fixture(params=["4", "2", "1"])
+def nv(request, monkeypatch):
+    monkeypatch.setenv("RS_AMD_NV", request.param)
+    return int(request.param)
+
+
+# ------------------------------------------------------------ golden vectors
+@pytest.mark.parametrize("flags", [0, 3])
+def test_mul_kats(flags):
+    """Generic.zig:402-455 through the device mulScalar shim."""
+    for c in load("engine_kats.json")["mul"]:
+        buf = bytearray([c["lo"]] * 32 + [c["hi"]] * 32)
+        R.engine_mul_scalar(buf, c["log_m"], flags)
+        assert list(buf[:32]) == [c["expected_lo"]] * 32
+        assert list(buf[32:]) == [c["expected_hi"]] * 32
+
+
+def test_encode_golden_rs16_16():
+    """tests.zig:104-129 + encode_data.zon, through the one-shot host API."""
+    fx = load("rs16_16_encode.json")
+    data = iota_input(16)
+    rec = R.encode(16, 16, [bytes(r) for r in data])
+    assert [list(r) for r in rec] == fx["parity"]
+
+
+@pytest.mark.parametrize("km", ["4,2", "10,4", "16,16", "32,32", "200,55"])
+@pytest.mark.parametrize("mode", ["corrected", "ref_literal"])
+def test_parity_digests(km, mode):
+    d = load("survey_digests.json")
+    k, m = map(int, km.split(","))
+    par = gpu_encode(k, m, survey_input(k)[None], 0 if mode == "corrected" else 3)
+    assert digest(par[0].tobytes()) == d["parity"][km][mode]
+
+
+def test_exhaustive_rs5_5_roundtrip():
+    """tests.zig:61-102: all 2^10 presence masks, one-shot host API."""
+    k = m = 5
+    orig = [bytes(r) for r in iota_input(k)]
+    rec = R.encode(k, m, orig)
+    ok = 0
+    for mask in range(1 << (k + m)):
+        o = [None if mask >> i & 1 else orig[i] for i in range(k)]
+        r = [None if mask >> (k + i) & 1 else rec[i] for i in range(m)]
+        if bin(mask).count("1") <= k:
+            assert R.decode(k, m, o, r) == orig, mask
+            ok += 1
+        else:
+            with pytest.raises(R.NotEnoughShards):
+                R.decode(k, m, o, r)
+    assert ok == 638
+
+
+# ------------------------------------------------------------ engine seam
+@pytest.mark.parametrize("flags", [0, 1])
+@pytest.mark.parametrize("case", [
+    # (shard_count, pos, size, trunc, skew_delta)
+    (4, 0, 4, 4, 4), (4, 0, 4, 3, 8), (8, 4, 4, 2, 12), (16, 0, 16, 14, 0), (16, 0, 16, 16, 0),
+    (8, 0, 8, 8, 0), (8, 0, 8, 5, 16), (2, 0, 2, 2, 2), (32, 0, 32, 20, 0), (64, 0, 64, 64, 64),
+    (512, 0, 512, 456, 0), (6, 2, 4, 4, 300), (2, 0, 2, 1, 1000),
+])
+def test_engine_fft_ifft_vs_oracle(oracle, flags, case):
+    count, pos, size, trunc, sd = case
+    rng = np.random.default_rng(count * 31 + sd)
+    for sb in (64, 192):
+        shards = rng.integers(0, 256, (count, sb), dtype=np.uint8)
+        for inverse in (False, True):
+            g = bytearray(shards.tobytes())
+            R.engine_fft(g, count, sb, pos, size, trunc, sd, flags, inverse)
+            o = shards.copy()
+            (oracle.ifft if inverse else oracle.fft)(o, pos, size, trunc, sd, flags)
+            assert bytes(g) == o.tobytes(), (case, sb, inverse)
+
+
+def test_engine_mul_scalar_random(oracle):
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 256, 64 * 33, dtype=np.uint8)
+    for lm in (0, 1, 257, 0x7777, 0xABCD, 65534, 65535):
+        for flags in (0, 1):
+            g = bytearray(x.tobytes())
+            R.engine_mul_scalar(g, lm, flags)
+            o = x.copy()
+            oracle.mul_scalar(o, lm, flags)
+            assert bytes(g) == o.tobytes(), (lm, flags)
+
+
+# ------------------------------------------------------------ codec vs oracle
+KM_SMALL = [(1, 1), (2, 1), (4, 2), (3, 4), (5, 5), (10, 4), (8, 4), (12, 4), (6, 3), (9, 8), (16, 16),
+            (17, 16), (20, 16), (16, 8), (30, 2), (64, 64), (100, 20), (200, 55), (33, 32)]
+
+
+@pytest.mark.parametrize("k,m", KM_SMALL)
+@pytest.mark.parametrize("flags", [0, 3])
+def test_encode_vs_oracle(oracle, nv, k, m, flags):
+    rng = np.random.default_rng(k * 7919 + m * 31 + flags)
+    n, sb = 3, 64 * 5
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = gpu_encode(k, m, data, flags)
+    for s in range(n):
+        st, exp = oracle.encode(k, m, data[s], flags)
+        assert st == 0
+        assert (par[s] == exp).all(), (k, m, s, R.encode_kernel_name(k, m, sb))
+
+
+@pytest.mark.parametrize("k,m", KM_SMALL)
+def test_reconstruct_vs_oracle(oracle, nv, k, m):
+    rng = np.random.default_rng(k * 104729 + m)
+    n, sb = 2, 64 * 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data)
+    for trial in range(3):
+        lost = list(rng.choice(k + m, size=min(m, k), replace=False))
+        if not any(i < k for i in lost):
+            lost[0] = int(rng.integers(0, k))
+        present = np.ones(k + m, np.uint8)
+        present[lost] = 0
+        missing = [i for i in range(k) if not present[i]]
+        got = gpu_reconstruct(k, m, present, data, par)
+        assert (got == data[:, missing]).all(), (k, m, trial, R.reconstruct_kernel_name(k, m, sb))
+        # and the oracle agrees with itself through the same API
+        exp = oracle.reconstruct_batch(k, m, present, np.concatenate([data, par], axis=1))
+        assert (got == exp).all()
+
+
+def test_reconstruct_not_enough_shards():
+    data = np.zeros((1, 10, 64), np.uint8)
+    par = np.zeros((1, 4, 64), np.uint8)
+    present = np.ones(14, np.uint8)
+    present[:5] = 0
+    with pytest.raises(R.NotEnoughShards):
+        gpu_reconstruct(10, 4, present, data, par)
+
+
+def test_strided_and_unaligned_layouts(oracle):
+    """Non-packed stripe strides and 4-byte-aligned (not 16) bases -> narrower lanes, same bytes."""
+    rng = np.random.default_rng(9)
+    k, m, sb, n = 10, 4, 1024, 5
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = oracle.encode_batch(k, m, data)
+    big = torch.zeros((n, k * sb + 4 + 64), dtype=torch.uint8, device=DEV)
+    big[:, 4:4 + k * sb] = to_dev(data.reshape(n, -1))
+    par = torch.zeros((n, m * sb + 8), dtype=torch.uint8, device=DEV)
+    st = R.lib().rs_encode_batch_dev(k, m, sb, n, big.data_ptr() + 4, big.stride(0), par.data_ptr() + 4,
+                                     par.stride(0), 0, None)
+    assert st == 0, R.lib().rs_last_error()
+    torch.cuda.synchronize()
+    got = par[:, 4:4 + m * sb].cpu().numpy().reshape(n, m, sb)
+    assert (got == exp).all()
+
+
+# ------------------------------------------------------------ BASELINE sizes
+def sample_columns(oracle, k, m, data, par, cols, flags=0):
+    for s, c in cols:
+        col = np.ascontiguousarray(data[s][:, 64 * c:64 * (c + 1)])
+        st, exp = oracle.encode(k, m, col, flags)
+        assert st == 0
+        assert (par[s][:, 64 * c:64 * (c + 1)] == exp).all(), (s, c)
+
+
+@pytest.mark.parametrize("k,m,sb,n,erase", [
+    (10, 4, 1 << 20, 24, [0, 1, 2, 3]),       # configs[1]/[2] shape (fewer stripes)
+    (4, 2, 64 << 10, 1, [1, 3]),              # configs[0]
+    (200, 55, 256 << 10, 2, list(range(0, 110, 2))),  # configs[4]
+])
+def test_baseline_shapes_roundtrip(oracle, k, m, sb, n, erase):
+    data = splitmix_bytes(0x5EED0000, n * k * sb).reshape(n, k, sb)
+    par = gpu_encode(k, m, data)
+    rng = np.random.default_rng(1)
+    L = sb // 64
+    cols = [(int(rng.integers(0, n)), int(c)) for c in rng.integers(0, L, 24)] + [(n - 1, L - 1), (0, 0)]
+    sample_columns(oracle, k, m, data, par, cols)
+    if k * sb <= (64 << 10) * 4:  # small config: full oracle comparison
+        exp = oracle.encode_batch(k, m, data)
+        assert (par == exp).all()
+    present = np.ones(k + m, np.uint8)
+    present[erase] = 0
+    got = gpu_reconstruct(k, m, present, data, par)
+    assert (got == data[:, erase]).all()
+    # erase recovery shards too (any m of k+m)
+    present = np.ones(k + m, np.uint8)
+    lost = list(rng.choice(k, size=m // 2, replace=False)) + [k + i for i in range(m - m // 2)]
+    present[lost] = 0
+    missing = [i for i in range(k) if not present[i]]
+    got = gpu_reconstruct(k, m, present, data, par)
+    assert (got == data[:, missing]).all()
+
+
+def test_linearity_full_size():
+    """encode(a ^ b) == encode(a) ^ encode(b) at RS(10,4) 1 MiB (GF(2)-linearity)."""
+    k, m, sb, n = 10, 4, 1 << 20, 4
+    a = splitmix_bytes(11, n * k * sb).reshape(n, k, sb)
+    b = splitmix_bytes(12, n * k * sb).reshape(n, k, sb)
+    pa, pb, pab = gpu_encode(k, m, a), gpu_encode(k, m, b), gpu_encode(k, m, a ^ b)
+    assert ((pa ^ pb) == pab).all()
+
+
+def test_repeatable_and_nan_free_of_state():
+    """Same inputs -> same bytes across calls and plan-cache hits."""
+    k, m, sb = 10, 4, 1 << 16
+    d = splitmix_bytes(3, 8 * k * sb).reshape(8, k, sb)
+    assert (gpu_encode(k, m, d) == gpu_encode(k, m, d)).all()
