@@ -363,11 +363,13 @@ dim3 grid_for(uint64_t shard_bytes, int nv, uint64_t n_stripes) {
 }  // namespace
 
 // ---------------------------------------------------------------- selection
-// Instantiated register variants: (size, NV) with size*2*NV VGPRs of live state
-// kept <= 128 per lane for encode (acc + one chunk) and decode (W slots).
+// Instantiated register variants (see launch_*): encode keeps acc + one chunk
+// (2*C slots) live with 2*C*2*NV <= 64 VGPRs of state; decode keeps W slots,
+// W*2*NV <= 128.
 static int clamp_nv(int nv, int size, bool enc) {
   const int live = enc ? 2 * size : size;  // symbol slots live at once
-  while (nv > 1 && live * 2 * nv > 128) nv >>= 1;
+  const int limit = enc ? 64 : 128;
+  while (nv > 1 && live * 2 * nv > limit) nv >>= 1;
   return nv;
 }
 

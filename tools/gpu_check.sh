@@ -18,5 +18,11 @@ run pytest_gpu 420 python -m pytest tests $PYTEST_ARGS
 rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stop: pytest rc=$rc"; exit $rc; fi
 run smoke 200 python __graft_entry__.py smoke || exit $?
-run bench 300 python bench.py ${BENCH_ARGS:-"--steps 5 --warmup 2 --cpu-seconds 8"} || exit $?
+run bench 300 python bench.py ${BENCH_ARGS:---steps 5 --warmup 2 --cpu-seconds 8} || exit $?
+if [ -n "$PROFILE" ]; then
+  R=$(pwd)
+  export TMPDIR=/tmp
+  run rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- \
+      python3 "$R/bench.py" ${PROF_ARGS:---steps 5 --warmup 2 --cpu-seconds 0} || exit $?
+fi
 exit $rc
