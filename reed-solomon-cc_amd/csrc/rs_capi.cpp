@@ -116,8 +116,9 @@ struct EncodePlan {
 
 struct DecodePlan {
   std::shared_ptr<DevBuf> buf;
-  uint32_t work, chunk, trunc, e;
-  size_t off_fft, off_pre, off_post, off_src, off_dst;  // byte offsets into buf
+  bool matrix = false;
+  uint32_t work = 0, chunk = 0, trunc = 0, e = 0, n_in = 0;
+  size_t off_fft = 0, off_pre = 0, off_post = 0, off_src = 0, off_dst = 0, off_mat = 0;  // byte offsets into buf
 };
 
 std::mutex g_plan_mu;
@@ -172,11 +173,41 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   return RS_OK;
 }
 
-// root.zig:268-335 erasure pattern -> evalPoly -> masks and table block
+// Multiplies the FFT reconstruct performs for a pattern (plan-time estimate used to
+// choose between the FFT kernels and the matrix kernel).
+uint64_t fft_decode_mul_count(uint64_t k, uint64_t m, uint64_t present_count, uint64_t e) {
+  const uint64_t C = ceil_pow2(m), end = C + k, W = ceil_pow2(C + k);
+  const uint16_t *sk = tables().skew;
+  auto live = [&](uint64_t idx) -> uint64_t { return idx < kModulus && sk[idx] != kModulus ? 1 : 0; };
+  auto group = [&](uint64_t r, uint64_t d) {  // m01 + m23 over d pairs, m02 over 2d
+    const uint64_t b = r + d - 1;
+    return d * (live(b) + live(b + 2 * d)) + 2 * d * live(b + d);
+  };
+  uint64_t n = present_count + e;  // erasure masks + reveal (root.zig:292-303, 321-326)
+  uint64_t d = 1;                  // IFFT, Generic.zig:80-147
+  for (uint64_t d4 = 4; d4 <= W; d = d4, d4 <<= 2)
+    for (uint64_t r = 0; r < end; r += d4) n += group(r, d);
+  if (d < W) n += d * live(d - 1);
+  uint64_t d4 = W;  // FFT, Generic.zig:15-78
+  for (uint64_t dd = W >> 2; dd != 0; d4 = dd, dd >>= 2)
+    for (uint64_t r = 0; r < end; r += d4) n += group(r, dd);
+  if (d4 == 2)
+    for (uint64_t r = 0; r < end; r += 2) n += live(r);
+  return n;
+}
+
+const char *decode_mode_env() {
+  const char *e = std::getenv("RS_AMD_DECODE");
+  return e ? e : "auto";
+}
+
+// root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
+// kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present,
                     std::shared_ptr<DecodePlan> &out) {
+  const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                    std::to_string(flags) + "/";
+                    std::to_string(flags) + "/" + mode + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::lock_guard<std::mutex> lk(g_plan_mu);
@@ -187,16 +218,72 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
   }
   const bool d1 = flags & RS_FLAG_QUIRK_D1;
   const uint64_t C = ceil_pow2(m), end = C + k, W = ceil_pow2(C + k);
+  uint64_t e = 0, present_count = 0;
+  for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+  for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
+  const bool can_matrix = e >= 1 && e <= kMatrixMaxOut;
+  bool use_matrix = can_matrix && 3 * k * e <= 4 * fft_decode_mul_count(k, m, present_count, e);
+  if (mode == "fft") use_matrix = false;
+  if (mode == "matrix") use_matrix = can_matrix;
+
+  auto plan = std::make_shared<DecodePlan>();
+  plan->work = static_cast<uint32_t>(W);
+  plan->chunk = static_cast<uint32_t>(C);
+  plan->trunc = static_cast<uint32_t>(end);
+
+  if (use_matrix) {
+    // inputs: every present original + the first e present recovery shards (exactly k)
+    std::vector<uint8_t> received(W, 0);
+    std::vector<uint64_t> in_pos, out_pos;
+    std::vector<int32_t> src;
+    for (uint64_t i = 0; i < k; i++)
+      if (present[i]) {
+        received[C + i] = 1;
+        in_pos.push_back(C + i);
+        src.push_back(static_cast<int32_t>(i));
+      } else {
+        out_pos.push_back(C + i);
+      }
+    for (uint64_t r = 0; r < m && in_pos.size() < k; r++)
+      if (present[k + r]) {
+        received[r] = 1;
+        in_pos.push_back(r);
+        src.push_back(kSrcRecovery | static_cast<int32_t>(r));
+      }
+    std::vector<uint16_t> er(kOrder);
+    erasure_logs(received.data(), k, m, er.data());
+    const size_t n_in = in_pos.size(), n_out = out_pos.size();
+    std::vector<uint16_t> img(n_in * n_out * 16);
+    std::vector<uint16_t> sym(W);
+    for (size_t t = 0; t < n_in; t++)
+      for (int b = 0; b < 16; b++) {  // images of basis symbol 1<<b at input t
+        std::fill(sym.begin(), sym.end(), 0);
+        sym[in_pos[t]] = static_cast<uint16_t>(1u << b);
+        scalar_reconstruct(sym.data(), received.data(), er.data(), k, m, d1);
+        for (size_t j = 0; j < n_out; j++) img[(t * n_out + j) * 16 + b] = sym[out_pos[j]];
+      }
+    std::vector<RsTab> tabs(n_in * n_out);
+    for (size_t i = 0; i < n_in * n_out; i++) tabs[i] = make_tab_from_images(&img[i * 16]);
+    std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + n_in * sizeof(int32_t));
+    std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
+    std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), src.data(), n_in * sizeof(int32_t));
+    int st = upload(blob.data(), blob.size(), dev, plan->buf);
+    if (st) return st;
+    plan->matrix = true;
+    plan->e = static_cast<uint32_t>(n_out);
+    plan->n_in = static_cast<uint32_t>(n_in);
+    plan->off_mat = 0;
+    plan->off_src = tabs.size() * sizeof(RsTab);
+    g_dec_plans.emplace(key, plan);
+    out = plan;
+    return RS_OK;
+  }
+
   std::vector<uint8_t> received(W, 0);
   for (uint64_t i = 0; i < m; i++) received[i] = present[k + i] ? 1 : 0;
   for (uint64_t i = 0; i < k; i++) received[C + i] = present[i] ? 1 : 0;
   std::vector<uint16_t> er(kOrder, 0);
-  for (uint64_t i = 0; i < m; i++)  // root.zig:278-287
-    if (!received[i]) er[i] = 1;
-  for (uint64_t i = m; i < C; i++) er[i] = 1;
-  for (uint64_t i = C; i < end; i++)
-    if (!received[i]) er[i] = 1;
-  eval_poly(er.data(), end);  // root.zig:289
+  erasure_logs(received.data(), k, m, er.data());  // root.zig:277-289
 
   std::vector<RsTab> tabs;
   push_ifft_tabs(tabs, W, 0, d1);
@@ -205,7 +292,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
   const size_t n_fft = tabs.size() - n_ifft;
   std::vector<int32_t> src(W, -1), dst(W, -1);
   std::vector<RsTab> pre(W), post(W);
-  uint32_t e = 0;
+  uint32_t ne = 0;
   for (uint64_t p = 0; p < W; p++) {
     if (p < m && received[p]) {
       src[p] = kSrcRecovery | static_cast<int32_t>(p);
@@ -215,7 +302,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
       pre[p] = make_tab(er[p], d1);
     }
     if (p >= C && p < end && !received[p]) {
-      dst[p] = static_cast<int32_t>(e++);
+      dst[p] = static_cast<int32_t>(ne++);
       post[p] = make_tab(static_cast<uint16_t>(kModulus - er[p]), d1);  // root.zig:321-326
     }
   }
@@ -226,13 +313,9 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
   const size_t off_src = tabs.size() * sizeof(RsTab), off_dst = off_src + W * sizeof(int32_t);
   std::memcpy(blob.data() + off_src, src.data(), W * sizeof(int32_t));
   std::memcpy(blob.data() + off_dst, dst.data(), W * sizeof(int32_t));
-  auto plan = std::make_shared<DecodePlan>();
   int st = upload(blob.data(), blob.size(), dev, plan->buf);
   if (st) return st;
-  plan->work = static_cast<uint32_t>(W);
-  plan->chunk = static_cast<uint32_t>(C);
-  plan->trunc = static_cast<uint32_t>(end);
-  plan->e = e;
+  plan->e = ne;
   plan->off_fft = n_ifft * sizeof(RsTab);
   plan->off_pre = (n_ifft + n_fft) * sizeof(RsTab);
   plan->off_post = plan->off_pre + W * sizeof(RsTab);
@@ -374,7 +457,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   if ((st = current_device(&dev))) return st;
   std::shared_ptr<DecodePlan> plan;
   if ((st = get_decode_plan(dev, k, m, flags, present, plan))) return st;
-  const KernelChoice kc = choose_decode(k, m, sb, max_nv);
+  const KernelChoice kc = plan->matrix ? choose_decode_matrix(plan->e, max_nv) : choose_decode(k, m, sb, max_nv);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint8_t *base = static_cast<const uint8_t *>(plan->buf->p);
   DecodeArgs a{};
@@ -393,9 +476,12 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   a.pos_dst = reinterpret_cast<const int32_t *>(base + plan->off_dst);
   a.work = plan->work;
   a.trunc = plan->trunc;
+  a.tab_mat = reinterpret_cast<const RsTab *>(base + plan->off_mat);
+  a.n_in = plan->n_in;
+  a.n_out = plan->e;
   if (!a.orig) a.orig = a.rec;  // never dereferenced for absent shards
   if (!a.rec) a.rec = a.orig;
-  if (kc.variant == Variant::kRegister) {
+  if (kc.variant != Variant::kGeneric) {
     a.n_stripes = n_stripes;
     HIP_TRY(launch_decode(kc, a, s));
     return RS_OK;

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <vector>
 
 namespace rs {
 
@@ -82,28 +83,116 @@ uint64_t ceil_pow2(uint64_t v) {
   return p;
 }
 
-RsTab make_tab(uint16_t log_m, bool quirk_d1) {
-  // field f: bit offset in x and width; tables hold byte_o(mul16(v << off, log_m)).
+uint16_t mul_engine(uint16_t x, uint16_t log_m, bool quirk_d1) {
+  if (!quirk_d1) return mul16(x, log_m);
+  // Generic.zig:283 (D1): prod_hi uses t1_hi[lo & 15], i.e. the hi byte of
+  // mul(((lo & 15) << 4) ^ (x & 0xFFF0)) — still GF(2)-linear in x.
+  const uint16_t xh = static_cast<uint16_t>(((x & 0xF) << 4) ^ (x & 0xFFF0));
+  return static_cast<uint16_t>((mul16(x, log_m) & 0xFF) | (mul16(xh, log_m) & 0xFF00));
+}
+
+RsTab make_tab_from_images(const uint16_t images[16]) {
+  // field f: bit offset in x and width; tables hold byte_o(map(v << off)).
   static constexpr int kOff[6] = {0, 3, 6, 8, 11, 14};
   static constexpr int kBits[6] = {3, 3, 2, 3, 3, 2};
   static constexpr int kSlot[6] = {0, 2, 4, 5, 7, 9};
   RsTab t{};
   for (int f = 0; f < 6; f++) {
     for (uint32_t v = 0; v < (1u << kBits[f]); v++) {
-      const uint16_t x = static_cast<uint16_t>(v << kOff[f]);
-      // Generic.zig:283 (D1): prod_hi uses t1_hi[lo & 15], i.e. the hi byte of
-      // mul(((lo & 15) << 4) ^ (x & 0xFFF0)) — a different GF(2)-linear map.
-      const uint16_t xh = quirk_d1 ? static_cast<uint16_t>(((x & 0xF) << 4) ^ (x & 0xFFF0)) : x;
-      const uint32_t plo = mul16(x, log_m) & 0xFF;
-      const uint32_t phi = mul16(xh, log_m) >> 8;
+      uint16_t p = 0;
+      for (int b = 0; b < kBits[f]; b++)
+        if (v >> b & 1) p ^= images[kOff[f] + b];
       const int w = kSlot[f] + (v >> 2), sh = 8 * (v & 3);
-      t.lo[w] |= plo << sh;
-      t.hi[w] |= phi << sh;
+      t.lo[w] |= static_cast<uint32_t>(p & 0xFF) << sh;
+      t.hi[w] |= static_cast<uint32_t>(p >> 8) << sh;
     }
   }
+  return t;
+}
+
+RsTab make_tab(uint16_t log_m, bool quirk_d1) {
+  uint16_t img[16];
+  for (int b = 0; b < 16; b++) img[b] = mul_engine(static_cast<uint16_t>(1u << b), log_m, quirk_d1);
+  RsTab t = make_tab_from_images(img);
   t.flags = 0;
   t.log_m = log_m;
   return t;
+}
+
+namespace {
+// scalar butterflies (Generic.zig:149-192) and transforms (15-147), pos = 0
+inline void fft_bf_s(uint16_t &x, uint16_t &y, uint16_t lm, bool q) {
+  if (lm != kModulus) x ^= mul_engine(y, lm, q);
+  y ^= x;
+}
+inline void ifft_bf_s(uint16_t &x, uint16_t &y, uint16_t lm, bool q) {
+  y ^= x;
+  if (lm != kModulus) x ^= mul_engine(y, lm, q);
+}
+void scalar_ifft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool q) {
+  const uint16_t *sk = tables().skew;
+  uint64_t d = 1;
+  for (uint64_t d4 = 4; d4 <= size; d = d4, d4 <<= 2)
+    for (uint64_t r = 0; r < trunc; r += d4) {
+      const uint64_t b = r + d + sd - 1;
+      const uint16_t m01 = sk[b], m02 = sk[b + d], m23 = sk[b + 2 * d];
+      for (uint64_t i = r; i < r + d; i++) {
+        ifft_bf_s(s[i], s[i + d], m01, q);
+        ifft_bf_s(s[i + 2 * d], s[i + 3 * d], m23, q);
+        ifft_bf_s(s[i], s[i + 2 * d], m02, q);
+        ifft_bf_s(s[i + d], s[i + 3 * d], m02, q);
+      }
+    }
+  if (d < size) {
+    const uint16_t lm = sk[d + sd - 1];
+    for (uint64_t i = 0; i < d; i++) ifft_bf_s(s[i], s[d + i], lm, q);
+  }
+}
+void scalar_fft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool q) {
+  const uint16_t *sk = tables().skew;
+  uint64_t d4 = size;
+  for (uint64_t d = size >> 2; d != 0; d4 = d, d >>= 2)
+    for (uint64_t r = 0; r < trunc; r += d4) {
+      const uint64_t b = r + d + sd - 1;
+      const uint16_t m01 = sk[b], m02 = sk[b + d], m23 = sk[b + 2 * d];
+      for (uint64_t i = r; i < r + d; i++) {
+        fft_bf_s(s[i], s[i + 2 * d], m02, q);
+        fft_bf_s(s[i + d], s[i + 3 * d], m02, q);
+        fft_bf_s(s[i], s[i + d], m01, q);
+        fft_bf_s(s[i + 2 * d], s[i + 3 * d], m23, q);
+      }
+    }
+  if (d4 == 2)
+    for (uint64_t r = 0; r < trunc; r += 2) fft_bf_s(s[r], s[r + 1], sk[r + sd], q);
+}
+}  // namespace
+
+void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *er) {
+  const uint64_t C = ceil_pow2(m), end = C + k;
+  std::memset(er, 0, kOrder * sizeof(uint16_t));
+  for (uint64_t i = 0; i < m; i++)
+    if (!received[i]) er[i] = 1;
+  for (uint64_t i = m; i < C; i++) er[i] = 1;
+  for (uint64_t i = C; i < end; i++)
+    if (!received[i]) er[i] = 1;
+  eval_poly(er, end);
+}
+
+void scalar_reconstruct(uint16_t *sym, const uint8_t *received, const uint16_t *er, uint64_t k, uint64_t m,
+                        bool q) {
+  const uint64_t C = ceil_pow2(m), end = C + k, W = ceil_pow2(C + k);
+  for (uint64_t i = 0; i < W; i++) {
+    const bool live = (i < m || (i >= C && i < end)) && received[i];
+    sym[i] = live ? mul_engine(sym[i], er[i], q) : 0;
+  }
+  scalar_ifft(sym, W, end, 0, q);
+  for (uint64_t i = 1; i < W; i++) {
+    const uint64_t w = i & (~i + 1);
+    for (uint64_t j = 0; j < w; j++) sym[i - w + j] ^= sym[i + j];
+  }
+  scalar_fft(sym, W, end, 0, q);
+  for (uint64_t i = C; i < end; i++)
+    if (!received[i]) sym[i] = mul_engine(sym[i], static_cast<uint16_t>(kModulus - er[i]), q);
 }
 
 RsTab make_twiddle(uint32_t skew_index, bool quirk_d1) {

@@ -55,9 +55,26 @@ inline uint16_t sub_mod(uint32_t x, uint32_t y) {  // utilities.zig:15-18
 }
 uint16_t mul16(uint16_t x, uint16_t log_m);  // utilities.zig:5-8
 
+// v_perm tables for an arbitrary GF(2)-linear map on 16-bit symbols, given the
+// images of the 16 basis symbols 1 << b.
+RsTab make_tab_from_images(const uint16_t images[16]);
 // v_perm tables for multiplication by exp[log_m]; quirk_d1 reproduces
 // Generic.zig:283 (hi product of nibble 0 read from t1_hi).
 RsTab make_tab(uint16_t log_m, bool quirk_d1);
+// The engine's multiply as a scalar map (Generic.zig:275-298, with D1 if asked).
+uint16_t mul_engine(uint16_t x, uint16_t log_m, bool quirk_d1);
+
+// ---- scalar (one symbol per position) restatement of the codec, used only to
+// derive reconstruct matrices at plan time (host, per erasure pattern).
+// Applies the reconstruct of root.zig:268-335 to W = ceilPow2(chunk+k) symbols:
+// sym[pos] holds the received symbols (recovery at [0,m), originals at
+// [chunk, chunk+k)); `received` flags positions; on return the missing
+// originals hold their restored symbols. `erasures` = evalPoly output for the
+// pattern (root.zig:277-289), computed once by the caller.
+void scalar_reconstruct(uint16_t *sym, const uint8_t *received, const uint16_t *erasures, uint64_t k, uint64_t m,
+                        bool quirk_d1);
+// root.zig:277-289: erasure flags for a received pattern -> evalPoly -> logs (65536 entries)
+void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *out);
 // Table for an FFT/IFFT twiddle: XOR-only marker when log_m == 65535
 // (the engine's `log_m == gf.modulus` shortcut, Generic.zig:38,47,53,103,...).
 RsTab make_twiddle(uint32_t skew_index, bool quirk_d1);

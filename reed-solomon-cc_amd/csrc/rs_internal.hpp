@@ -56,13 +56,18 @@ struct DecodeArgs {
   uint32_t trunc;  // chunk + k
   uint8_t *scratch;  // generic path only: [stripe][W][sb]
   uint64_t scratch_stripes;
+  // matrix variant: restored[j] = XOR_i map_ij(in[i]) over n_in received shards
+  // pos_src[0..n_in) = sources, tab_mat[i * n_out + j] = map_ij (GF(2)-linear)
+  const RsTab *tab_mat;
+  uint32_t n_in;
+  uint32_t n_out;
 };
 constexpr int32_t kSrcRecovery = 0x40000000;
 constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
 
 // Kernel variants: fused register-resident for small transforms, generic
 // (per-lane column walk over an HBM scratch work buffer) otherwise.
-enum class Variant { kRegister, kGeneric };
+enum class Variant { kRegister, kGeneric, kMatrix };
 
 struct KernelChoice {
   Variant variant;
@@ -74,6 +79,9 @@ struct KernelChoice {
 // max_nv: widest per-lane access (1, 2, 4 dword pairs) the pointer/stride alignment allows
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
+// reconstruct as an n_out x n_in matrix of GF(2)-linear maps (decode matrix + GF MAC)
+KernelChoice choose_decode_matrix(uint32_t n_out, int max_nv);
+constexpr uint32_t kMatrixMaxOut = 8;
 
 hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
 hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s);

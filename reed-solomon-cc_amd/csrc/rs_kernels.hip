@@ -138,6 +138,83 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
   }
 }
 
+// ================================================= matrix reconstruct (e <= 8)
+// restored_j = XOR_i M_ij(in_i): the reconstruct of root.zig:268-335 is
+// GF(2)-linear in the received shards, so for one erasure pattern it is an
+// n_out x n_in matrix of 16x16 GF(2) maps (host-derived, rs_capi.cpp). Each
+// input is read once; its six bit-field selectors are shared by all n_out
+// multiply-accumulates. Reads k shards, writes e: the algorithmic minimum.
+template <int NV>
+struct Sel {
+  uint32_t a0[NV], a1[NV], a2[NV], b0[NV], b1[NV], b2[NV];
+};
+
+template <int NV>
+__device__ __forceinline__ void make_sel(Sel<NV> &s, const Sym<NV> &y) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    s.a0[v] = y.l[v] & 0x07070707u;
+    s.a1[v] = (y.l[v] >> 3) & 0x07070707u;
+    s.a2[v] = (y.l[v] >> 6) & 0x03030303u;
+    s.b0[v] = y.h[v] & 0x07070707u;
+    s.b1[v] = (y.h[v] >> 3) & 0x07070707u;
+    s.b2[v] = (y.h[v] >> 6) & 0x03030303u;
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void mac_sel(Sym<NV> &x, const Sel<NV> &s, const Tab &t) {
+  using dev::perm;
+  using dev::xor3;
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    uint32_t l = xor3(x.l[v], perm(t.lo[1], t.lo[0], s.a0[v]), perm(t.lo[3], t.lo[2], s.a1[v]));
+    uint32_t h = xor3(x.h[v], perm(t.hi[1], t.hi[0], s.a0[v]), perm(t.hi[3], t.hi[2], s.a1[v]));
+    l = xor3(l, perm(t.lo[4], t.lo[4], s.a2[v]), perm(t.lo[6], t.lo[5], s.b0[v]));
+    h = xor3(h, perm(t.hi[4], t.hi[4], s.a2[v]), perm(t.hi[6], t.hi[5], s.b0[v]));
+    x.l[v] = xor3(l, perm(t.lo[8], t.lo[7], s.b1[v]), perm(t.lo[9], t.lo[9], s.b2[v]));
+    x.h[v] = xor3(h, perm(t.hi[8], t.hi[7], s.b1[v]), perm(t.hi[9], t.hi[9], s.b2[v]));
+  }
+}
+
+template <int E, int NV>
+__global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
+  uint64_t off;
+  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  const uint64_t sb = a.shard_bytes;
+  typedef const __attribute__((address_space(4))) int32_t *CI;
+  const CI srcs = (CI)(a.pos_src);
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
+    const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+    Sym<NV> acc[E];
+#pragma unroll
+    for (int j = 0; j < E; j++) dev::zero(acc[j]);
+    Sym<NV> y;
+    {
+      const int32_t src = srcs[0];
+      dev::load_sym(y, ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
+    }
+    for (uint32_t i = 0; i < a.n_in; i++) {
+      // software pipeline: issue the next input's load before this one's MACs
+      Sym<NV> nxt = y;
+      if (i + 1 < a.n_in) {
+        const int32_t src = srcs[i + 1];
+        dev::load_sym(nxt, ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
+      }
+      Sel<NV> sel;
+      make_sel(sel, y);
+      const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
+#pragma unroll
+      for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
+      y = nxt;
+    }
+    uint8_t *out = a.out + s * a.out_stripe_stride + off;
+#pragma unroll
+    for (int j = 0; j < E; j++) dev::store_sym(out + static_cast<uint64_t>(j) * sb, acc[j]);
+  }
+}
+
 // ============================================ generic: column walk in HBM scratch
 template <int NV>
 __device__ __forceinline__ void ld(Sym<NV> &s, const uint8_t *p) {
@@ -424,6 +501,29 @@ KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
   return {Variant::kGeneric, static_cast<int>(W), 1, "decode_generic_nv1"};
 }
 
+KernelChoice choose_decode_matrix(uint32_t n_out, int max_nv) {
+  static const char *kNames[9][3] = {
+      {"", "", ""},
+      {"decode_matrix_e1_nv1", "decode_matrix_e1_nv2", "decode_matrix_e1_nv4"},
+      {"decode_matrix_e2_nv1", "decode_matrix_e2_nv2", "decode_matrix_e2_nv4"},
+      {"decode_matrix_e3_nv1", "decode_matrix_e3_nv2", "decode_matrix_e3_nv4"},
+      {"decode_matrix_e4_nv1", "decode_matrix_e4_nv2", "decode_matrix_e4_nv4"},
+      {"decode_matrix_e5_nv1", "decode_matrix_e5_nv2", "decode_matrix_e5_nv4"},
+      {"decode_matrix_e6_nv1", "decode_matrix_e6_nv2", "decode_matrix_e6_nv4"},
+      {"decode_matrix_e7_nv1", "decode_matrix_e7_nv2", "decode_matrix_e7_nv4"},
+      {"decode_matrix_e8_nv1", "decode_matrix_e8_nv2", "decode_matrix_e8_nv4"}};
+  const int nv = std::min(env_nv(4), max_nv);
+  const int ni = nv == 1 ? 0 : nv == 2 ? 1 : 2;
+  return {Variant::kMatrix, static_cast<int>(n_out), nv, kNames[n_out][ni]};
+}
+
+#define RS_MAT_CASE(E_, NV_)                                                     \
+  if (kc.size == E_ && kc.nv == NV_) {                                           \
+    hipLaunchKernelGGL((k_decode_matrix<E_, NV_>), grid, dim3(kBlock), 0, s, a); \
+    return hipGetLastError();                                                    \
+  }
+#define RS_MAT_NV(E_) RS_MAT_CASE(E_, 1) RS_MAT_CASE(E_, 2) RS_MAT_CASE(E_, 4)
+
 #define RS_ENC_CASE(C_, NV_)                                                  \
   if (kc.size == C_ && kc.nv == NV_) {                                        \
     hipLaunchKernelGGL((k_encode_reg<C_, NV_>), grid, dim3(kBlock), 0, s, a); \
@@ -459,6 +559,11 @@ hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_
     RS_DEC_CASE(8, 1) RS_DEC_CASE(8, 2) RS_DEC_CASE(8, 4)
     RS_DEC_CASE(16, 1) RS_DEC_CASE(16, 2) RS_DEC_CASE(16, 4)
     RS_DEC_CASE(32, 1) RS_DEC_CASE(32, 2)
+    return hipErrorInvalidValue;
+  }
+  if (kc.variant == Variant::kMatrix) {
+    RS_MAT_NV(1) RS_MAT_NV(2) RS_MAT_NV(3) RS_MAT_NV(4)
+    RS_MAT_NV(5) RS_MAT_NV(6) RS_MAT_NV(7) RS_MAT_NV(8)
     return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(k_decode_generic<1>, grid, dim3(kBlock), 0, s, a);

@@ -54,6 +54,13 @@ def nv(request, monkeypatch):
     return int(request.param)
 
 
+@pytest.fixture(params=["fft", "matrix", "auto"])
+def decode_mode(request, monkeypatch):
+    """RS_AMD_DECODE: FFT kernels (root.zig:268-335 as written) or the e x k matrix kernel."""
+    monkeypatch.setenv("RS_AMD_DECODE", request.param)
+    return request.param
+
+
 # ------------------------------------------------------------ golden vectors
 @pytest.mark.parametrize("flags", [0, 3])
 def test_mul_kats(flags):
@@ -152,7 +159,7 @@ def test_encode_vs_oracle(oracle, nv, k, m, flags):
 
 
 @pytest.mark.parametrize("k,m", KM_SMALL)
-def test_reconstruct_vs_oracle(oracle, nv, k, m):
+def test_reconstruct_vs_oracle(oracle, nv, decode_mode, k, m):
     rng = np.random.default_rng(k * 104729 + m)
     n, sb = 2, 64 * 3
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
@@ -206,12 +213,13 @@ def sample_columns(oracle, k, m, data, par, cols, flags=0):
         assert (par[s][:, 64 * c:64 * (c + 1)] == exp).all(), (s, c)
 
 
+@pytest.mark.parametrize("decode_mode", ["fft", "auto"], indirect=True)
 @pytest.mark.parametrize("k,m,sb,n,erase", [
     (10, 4, 1 << 20, 24, [0, 1, 2, 3]),       # configs[1]/[2] shape (fewer stripes)
     (4, 2, 64 << 10, 1, [1, 3]),              # configs[0]
     (200, 55, 256 << 10, 2, list(range(0, 110, 2))),  # configs[4]
 ])
-def test_baseline_shapes_roundtrip(oracle, k, m, sb, n, erase):
+def test_baseline_shapes_roundtrip(oracle, decode_mode, k, m, sb, n, erase):
     data = splitmix_bytes(0x5EED0000, n * k * sb).reshape(n, k, sb)
     par = gpu_encode(k, m, data)
     rng = np.random.default_rng(1)
@@ -241,6 +249,25 @@ def test_linearity_full_size():
     b = splitmix_bytes(12, n * k * sb).reshape(n, k, sb)
     pa, pb, pab = gpu_encode(k, m, a), gpu_encode(k, m, b), gpu_encode(k, m, a ^ b)
     assert ((pa ^ pb) == pab).all()
+
+
+@pytest.mark.parametrize("flags", [0, 3])
+def test_reconstruct_matrix_ref_literal(oracle, monkeypatch, flags):
+    """The matrix kernel reproduces the FFT reconstruct bit for bit in both quirk modes
+    (the D1 multiply is GF(2)-linear, so its reconstruct is still a matrix of 16x16 maps)."""
+    rng = np.random.default_rng(77)
+    k, m, sb, n = 10, 4, 640, 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags)
+    present = np.ones(k + m, np.uint8)
+    present[[1, 4, 9, 11]] = 0
+    outs = {}
+    for mode in ("fft", "matrix"):
+        monkeypatch.setenv("RS_AMD_DECODE", mode)
+        outs[mode] = gpu_reconstruct(k, m, present, data, par, flags)
+    assert (outs["fft"] == outs["matrix"]).all()
+    exp = oracle.reconstruct_batch(k, m, present, np.concatenate([data, par], axis=1), quirks=flags)
+    assert (outs["fft"] == exp).all()
 
 
 def test_repeatable_and_nan_free_of_state():
