@@ -183,7 +183,7 @@ def main():
         enc_alg = (k + m) * sb * n  # algorithmic HBM bytes per encode launch
         rec_alg = (k + e) * sb * n  # k received shards read + e restored written
         kinds = {"encode": (enc_ms, enc_alg, R.encode_kernel_name(k, m, sb)),
-                 "reconstruct": (rec_ms, rec_alg, R.reconstruct_kernel_name(k, m, sb))}
+                 "reconstruct": (rec_ms, rec_alg, R.reconstruct_kernel_name(k, m, sb, present))}
         dom = max(kinds, key=lambda x: kinds[x][0])
         ms, alg, kname = kinds[dom]
         achieved = alg / (ms * 1e-3) / 1e9

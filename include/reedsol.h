@@ -100,8 +100,8 @@ typedef struct rs_decoder rs_decoder;
 int rs_decoder_new(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, rs_decoder **out);
 int rs_decoder_add_original_shard(rs_decoder *dec, uint64_t index, const uint8_t *shard, size_t len);
 int rs_decoder_add_recovery_shard(rs_decoder *dec, uint64_t index, const uint8_t *shard, size_t len);
-/* restored_out[k]: borrowed pointers; NULL for originals that were supplied
- * (the caller has them), restored data for the missing ones. */
+/* restored_out[k]: borrowed pointers to all k originals (supplied ones copied,
+ * missing ones restored), valid until the next decode / rs_decoder_free. */
 int rs_decoder_decode(rs_decoder *dec, const uint8_t **restored_out);
 void rs_decoder_free(rs_decoder *dec);
 
@@ -126,9 +126,12 @@ int rs_reconstruct_batch_dev(uint64_t original_count, uint64_t recovery_count, s
                              uint64_t recovery_stripe_stride, void *d_restored, uint64_t restored_stripe_stride,
                              uint32_t flags, rs_stream_t stream);
 
-/* Which device kernel a configuration runs on ("fused_reg_c4_nv4", "generic", ...). */
+/* Which device kernel a call would run on ("encode_reg_w4_nv4", "decode_matrix_e4_nv4",
+ * "encode_generic_nv1", ...), assuming 16-byte aligned buffers. present: k+m flags as
+ * for rs_reconstruct_batch_dev, or NULL for "the first min(k, m) originals lost". */
 const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
-const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
+const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                                       const uint8_t *present);
 
 /* ---------------------------------------- Engine seam (Generic.zig), test shim
  * The reference's comptime Engine interface (root.zig:10-12) at per-call

@@ -201,6 +201,19 @@ const char *decode_mode_env() {
   return e ? e : "auto";
 }
 
+constexpr uint32_t flags_none() { return 0; }
+
+// Matrix kernel when it does fewer multiplies than the FFT reconstruct
+// (k*e MACs at ~3/4 the cost of an FFT multiply: selectors shared across outputs).
+bool decode_uses_matrix(uint64_t k, uint64_t m, uint32_t flags, uint64_t e, uint64_t present_count) {
+  (void)flags;
+  const std::string mode = decode_mode_env();
+  const bool can_matrix = e >= 1 && e <= kMatrixMaxOut && (k + m) <= 4096;
+  if (mode == "fft") return false;
+  if (mode == "matrix") return can_matrix;
+  return can_matrix && 3 * k * e <= 4 * fft_decode_mul_count(k, m, present_count, e);
+}
+
 // root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
 // kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present,
@@ -221,10 +234,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
   uint64_t e = 0, present_count = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
-  const bool can_matrix = e >= 1 && e <= kMatrixMaxOut;
-  bool use_matrix = can_matrix && 3 * k * e <= 4 * fft_decode_mul_count(k, m, present_count, e);
-  if (mode == "fft") use_matrix = false;
-  if (mode == "matrix") use_matrix = can_matrix;
+  const bool use_matrix = decode_uses_matrix(k, m, flags, e, present_count);
 
   auto plan = std::make_shared<DecodePlan>();
   plan->work = static_cast<uint32_t>(W);
@@ -232,7 +242,11 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
   plan->trunc = static_cast<uint32_t>(end);
 
   if (use_matrix) {
-    // inputs: every present original + the first e present recovery shards (exactly k)
+    // inputs: every present original + the first e present recovery shards (exactly k:
+    // the unique restored data does not depend on which k). Under D1 the literal
+    // reconstruct is not a decoder, so its output depends on the pattern: keep ALL
+    // present shards then, exactly as the reference would receive them.
+    const uint64_t want = d1 ? present_count : k;
     std::vector<uint8_t> received(W, 0);
     std::vector<uint64_t> in_pos, out_pos;
     std::vector<int32_t> src;
@@ -244,7 +258,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
       } else {
         out_pos.push_back(C + i);
       }
-    for (uint64_t r = 0; r < m && in_pos.size() < k; r++)
+    for (uint64_t r = 0; r < m && in_pos.size() < want; r++)
       if (present[k + r]) {
         received[r] = 1;
         in_pos.push_back(r);
@@ -367,7 +381,19 @@ const uint16_t *rs_table_skew(void) { return tables().skew; }
 const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
 
 const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) { return choose_encode(k, m, sb, 4).name; }
-const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb) { return choose_decode(k, m, sb, 4).name; }
+const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const uint8_t *present) {
+  std::vector<uint8_t> def;
+  if (!present) {
+    def.assign(k + m, 1);
+    for (uint64_t i = 0; i < std::min(k, m); i++) def[i] = 0;
+    present = def.data();
+  }
+  uint64_t e = 0, have = 0;
+  for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+  for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
+  if (decode_uses_matrix(k, m, flags_none(), e, have)) return choose_decode_matrix(static_cast<uint32_t>(e), 4).name;
+  return choose_decode(k, m, sb, 4).name;
+}
 
 int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const void *d_original,
                         uint64_t orig_stride, void *d_recovery, uint64_t rec_stride, uint32_t flags,

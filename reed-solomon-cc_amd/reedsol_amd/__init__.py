@@ -78,7 +78,7 @@ def lib():
         "rs_encode_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32, vp]),
         "rs_reconstruct_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32, vp]),
         "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
-        "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz]),
+        "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_mul_scalar": (C.c_int, [vp, sz, C.c_uint16, u32]),
@@ -254,8 +254,11 @@ def encode_kernel_name(k, m, shard_bytes) -> str:
     return lib().rs_encode_kernel_name(k, m, shard_bytes).decode()
 
 
-def reconstruct_kernel_name(k, m, shard_bytes) -> str:
-    return lib().rs_reconstruct_kernel_name(k, m, shard_bytes).decode()
+def reconstruct_kernel_name(k, m, shard_bytes, present=None) -> str:
+    if present is None:
+        return lib().rs_reconstruct_kernel_name(k, m, shard_bytes, None).decode()
+    pres = (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
+    return lib().rs_reconstruct_kernel_name(k, m, shard_bytes, pres).decode()
 
 
 # ------------------------------------------------------------ engine test shims

@@ -79,8 +79,12 @@ def main():
     for v in variants:
         te, tr = float(np.median(res[v]["enc"])), float(np.median(res[v]["rec"]))
         os.environ["RS_AMD_NV"] = v[0]
+        if v[1]:
+            os.environ["RS_AMD_DECODE"] = v[1]
+        else:
+            os.environ.pop("RS_AMD_DECODE", None)
         row = {"nv": v[0], "decode": v[1] or "default",
-               "enc_kernel": R.encode_kernel_name(k, m, sb), "rec_kernel": R.reconstruct_kernel_name(k, m, sb),
+               "enc_kernel": R.encode_kernel_name(k, m, sb), "rec_kernel": R.reconstruct_kernel_name(k, m, sb, present),
                "enc_ms": round(te, 3), "enc_TBps": round(enc_bytes / te / 1e9, 3),
                "rec_ms": round(tr, 3), "rec_TBps": round(rec_bytes / tr / 1e9, 3),
                "enc_min_ms": round(min(res[v]["enc"]), 3), "rec_min_ms": round(min(res[v]["rec"]), 3)}
