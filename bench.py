@@ -24,6 +24,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "reed-solomon-cc_amd"))
 import reedsol_amd as R  # noqa: E402  (after torch: one HIP runtime)
+from reedsol_amd.sharding import all_ok, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -164,18 +165,13 @@ def main():
     t = time.perf_counter() - t0
     enc_ms = float(np.mean([ev[0].elapsed_time(ev[1]) for ev in events]))
     rec_ms = float(np.mean([ev[1].elapsed_time(ev[2]) for ev in events]))
-    if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+    t = max_over_ranks(t, device=dev)  # slowest rank sets the step time
+    enc_ms = max_over_ranks(enc_ms, device=dev)
+    rec_ms = max_over_ranks(rec_ms, device=dev)
 
     ok = None
     if not args.no_verify:
-        ok = bool(torch.equal(restored, data[:, erase]))
-    if world > 1:
-        okt = torch.tensor([1 if ok in (None, True) else 0], device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = None if args.no_verify else bool(okt.item())
+        ok = all_ok(bool(torch.equal(restored, data[:, erase])), device=dev)
 
     if rank == 0:
         data_bytes = k * sb * n  # per rank per op
