@@ -183,10 +183,13 @@ def main():
         dom = max(kinds, key=lambda x: kinds[x][0])
         ms, alg, kname = kinds[dom]
         achieved = alg / (ms * 1e-3) / 1e9
-        traffic = load_traffic([kname])
+        traffic = load_traffic([kname]) or {}
+        tr = traffic.get(kname)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": (traffic or {}).get(kname, {}).get("hbm_bytes_per_launch") if traffic else None,
+                    # HBM bytes per launch from PMC (profiles/traffic.json, per stripe x this batch)
+                    "traffic": int(tr["hbm_bytes_per_stripe"] * n) if tr else None,
+                    "traffic_source": tr["method"] + "; " + tr["workload"] if tr else None,
                     "kernel": kname, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ms, 4),
                     "per_kernel": {kk: {"kernel": v[2], "avg_ms": round(v[0], 4),
                                         "achieved_GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 1),
