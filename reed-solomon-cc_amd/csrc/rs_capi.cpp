@@ -391,7 +391,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   uint64_t e = 0, have = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
-  if (decode_uses_matrix(k, m, flags_none(), e, have)) return choose_decode_matrix(static_cast<uint32_t>(e), 4).name;
+  if (decode_uses_matrix(k, m, flags_none(), e, have)) return choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name;
   return choose_decode(k, m, sb, 4).name;
 }
 
@@ -483,7 +483,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   if ((st = current_device(&dev))) return st;
   std::shared_ptr<DecodePlan> plan;
   if ((st = get_decode_plan(dev, k, m, flags, present, plan))) return st;
-  const KernelChoice kc = plan->matrix ? choose_decode_matrix(plan->e, max_nv) : choose_decode(k, m, sb, max_nv);
+  const KernelChoice kc = plan->matrix ? choose_decode_matrix(plan->e, sb, max_nv) : choose_decode(k, m, sb, max_nv);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint8_t *base = static_cast<const uint8_t *>(plan->buf->p);
   DecodeArgs a{};

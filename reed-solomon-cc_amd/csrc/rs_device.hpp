@@ -197,19 +197,35 @@ struct VecT<4> {
   typedef uint32_t __attribute__((ext_vector_type(4))) type;
 };
 
+// NV = 1, 2 ("split"): the lane's lo dwords at p, hi dwords at p + 32 of one chunk.
+// NV = 4 ("contig"): a wave covers a 2 KiB region (32 chunks) with two loads of
+// 1 KiB contiguous each — lanes 0-31 read lo quarters, lanes 32-63 the matching hi
+// quarters — and one v_permlane32_swap per dword pairs every lane's lo with its hi
+// (p = the lane's first-load address, second load at p + 1024; see lane_offset).
 template <int NV>
 __device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__ p) {
   typedef typename VecT<NV>::type V;
-  const V lo = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
-  const V hi = __builtin_nontemporal_load(reinterpret_cast<const V *>(p + 32));
-  if constexpr (NV == 1) {
-    s.l[0] = lo;
-    s.h[0] = hi;
-  } else {
+  if constexpr (NV == 4) {
+    const V a = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
+    const V b = __builtin_nontemporal_load(reinterpret_cast<const V *>(p + 1024));
 #pragma unroll
-    for (int v = 0; v < NV; v++) {
-      s.l[v] = lo[v];
-      s.h[v] = hi[v];
+    for (int v = 0; v < 4; v++) {
+      const auto r = __builtin_amdgcn_permlane32_swap(a[v], b[v], false, false);
+      s.l[v] = r[0];
+      s.h[v] = r[1];
+    }
+  } else {
+    const V lo = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
+    const V hi = __builtin_nontemporal_load(reinterpret_cast<const V *>(p + 32));
+    if constexpr (NV == 1) {
+      s.l[0] = lo;
+      s.h[0] = hi;
+    } else {
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        s.l[v] = lo[v];
+        s.h[v] = hi[v];
+      }
     }
   }
 }
@@ -218,7 +234,17 @@ template <int NV>
 __device__ __forceinline__ void store_sym(uint8_t *__restrict__ p, const Sym<NV> &s) {
   typedef typename VecT<NV>::type V;
   V lo, hi;
-  if constexpr (NV == 1) {
+  if constexpr (NV == 4) {
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+      const auto r = __builtin_amdgcn_permlane32_swap(s.l[v], s.h[v], false, false);
+      lo[v] = r[0];
+      hi[v] = r[1];
+    }
+    __builtin_nontemporal_store(lo, reinterpret_cast<V *>(p));
+    __builtin_nontemporal_store(hi, reinterpret_cast<V *>(p + 1024));
+    return;
+  } else if constexpr (NV == 1) {
     lo = s.l[0];
     hi = s.h[0];
   } else {

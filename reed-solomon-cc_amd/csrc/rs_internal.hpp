@@ -80,7 +80,7 @@ struct KernelChoice {
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
 // reconstruct as an n_out x n_in matrix of GF(2)-linear maps (decode matrix + GF MAC)
-KernelChoice choose_decode_matrix(uint32_t n_out, int max_nv);
+KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv);
 constexpr uint32_t kMatrixMaxOut = 8;
 
 hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);

@@ -39,14 +39,21 @@ __host__ __device__ constexpr int ifft_tabs_ce(int size) {
   return n + (d < size ? 1 : 0);
 }
 
-// byte offset of this lane's dword pairs inside a shard; false if out of range
+// byte offset of this lane's data inside a shard (see dev::load_sym); false if
+// out of range. NV = 4 uses the contiguous 2 KiB-per-wave layout and needs
+// shard_bytes % 2048 == 0 (whole waves in range: the permlane swap needs all 64 lanes).
 template <int NV>
 __device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, uint64_t &off) {
   constexpr uint32_t kUnitsPerChunk = 8 / NV;
   const uint64_t unit = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const uint64_t units = shard_bytes / 64 * kUnitsPerChunk;
   if (unit >= units) return false;
-  off = unit / kUnitsPerChunk * 64 + unit % kUnitsPerChunk * (4 * NV);
+  if constexpr (NV == 4) {
+    const uint64_t lane = unit % 64;
+    off = unit / 64 * 2048 + (lane % 32) / 2 * 64 + (lane >= 32 ? 32 : 0) + (lane % 2) * 16;
+  } else {
+    off = unit / kUnitsPerChunk * 64 + unit % kUnitsPerChunk * (4 * NV);
+  }
   return true;
 }
 
@@ -478,9 +485,14 @@ static const char *reg_name(bool enc, int size, int nv) {
   return enc ? kEnc[si][ni] : kDec[si][ni];
 }
 
+// the NV = 4 lane layout covers 2 KiB per wave
+static int shard_nv(int max_nv, uint64_t shard_bytes) {
+  return (max_nv >= 4 && shard_bytes % 2048 != 0) ? 2 : max_nv;
+}
+
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
   (void)k;
-  (void)shard_bytes;
+  max_nv = shard_nv(max_nv, shard_bytes);
   const uint64_t C = ceil_pow2(m);
   if (C <= 16) {
     const int c = static_cast<int>(C);
@@ -491,7 +503,7 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
 }
 
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
-  (void)shard_bytes;
+  max_nv = shard_nv(max_nv, shard_bytes);
   const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
   if (W <= 32) {
     const int w = static_cast<int>(W);
@@ -501,7 +513,8 @@ KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
   return {Variant::kGeneric, static_cast<int>(W), 1, "decode_generic_nv1"};
 }
 
-KernelChoice choose_decode_matrix(uint32_t n_out, int max_nv) {
+KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv) {
+  max_nv = shard_nv(max_nv, shard_bytes);
   static const char *kNames[9][3] = {
       {"", "", ""},
       {"decode_matrix_e1_nv1", "decode_matrix_e1_nv2", "decode_matrix_e1_nv4"},

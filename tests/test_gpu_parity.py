@@ -147,9 +147,10 @@ KM_SMALL = [(1, 1), (2, 1), (4, 2), (3, 4), (5, 5), (10, 4), (8, 4), (12, 4), (6
 
 @pytest.mark.parametrize("k,m", KM_SMALL)
 @pytest.mark.parametrize("flags", [0, 3])
-def test_encode_vs_oracle(oracle, nv, k, m, flags):
+@pytest.mark.parametrize("sb", [320, 4096])  # 4096: whole 2 KiB waves -> NV=4 contiguous layout
+def test_encode_vs_oracle(oracle, nv, k, m, flags, sb):
     rng = np.random.default_rng(k * 7919 + m * 31 + flags)
-    n, sb = 3, 64 * 5
+    n = 3
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
     par = gpu_encode(k, m, data, flags)
     for s in range(n):
@@ -159,9 +160,10 @@ def test_encode_vs_oracle(oracle, nv, k, m, flags):
 
 
 @pytest.mark.parametrize("k,m", KM_SMALL)
-def test_reconstruct_vs_oracle(oracle, nv, decode_mode, k, m):
+@pytest.mark.parametrize("sb", [192, 2048])
+def test_reconstruct_vs_oracle(oracle, nv, decode_mode, k, m, sb):
     rng = np.random.default_rng(k * 104729 + m)
-    n, sb = 2, 64 * 3
+    n = 2
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
     par = oracle.encode_batch(k, m, data)
     for trial in range(3):
