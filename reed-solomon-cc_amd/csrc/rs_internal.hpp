@@ -74,6 +74,7 @@ struct KernelChoice {
   int size;  // chunk (encode) or W (decode) for register kernels
   int nv;    // dword pairs per lane
   const char *name;
+  int prefetch = 2;  // matrix kernel: inputs in flight per lane
 };
 
 // max_nv: widest per-lane access (1, 2, 4 dword pairs) the pointer/stride alignment allows

@@ -184,37 +184,42 @@ __device__ __forceinline__ void mac_sel(Sym<NV> &x, const Sel<NV> &s, const Tab 
   }
 }
 
-template <int E, int NV>
+template <int E, int NV, int D>
 __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
   uint64_t off;
   if (!lane_offset<NV>(a.shard_bytes, off)) return;
   const uint64_t sb = a.shard_bytes;
   typedef const __attribute__((address_space(4))) int32_t *CI;
   const CI srcs = (CI)(a.pos_src);
+  const uint32_t n_in = a.n_in;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+    auto in_ptr = [&](uint32_t i) {
+      const int32_t src = srcs[i];
+      return ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb;
+    };
     Sym<NV> acc[E];
 #pragma unroll
     for (int j = 0; j < E; j++) dev::zero(acc[j]);
-    Sym<NV> y;
-    {
-      const int32_t src = srcs[0];
-      dev::load_sym(y, ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
-    }
-    for (uint32_t i = 0; i < a.n_in; i++) {
-      // software pipeline: issue the next input's load before this one's MACs
-      Sym<NV> nxt = y;
-      if (i + 1 < a.n_in) {
-        const int32_t src = srcs[i + 1];
-        dev::load_sym(nxt, ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
-      }
-      Sel<NV> sel;
-      make_sel(sel, y);
-      const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
+    // prefetch ring: inputs i..i+D-1 in flight while input i is multiplied
+    Sym<NV> buf[D];
 #pragma unroll
-      for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
-      y = nxt;
+    for (int d = 0; d < D; d++)
+      if (static_cast<uint32_t>(d) < n_in) dev::load_sym(buf[d], in_ptr(d));
+    for (uint32_t i0 = 0; i0 < n_in; i0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; d++) {
+        const uint32_t i = i0 + d;
+        if (i >= n_in) break;
+        const Sym<NV> y = buf[d];
+        if (i + D < n_in) dev::load_sym(buf[d], in_ptr(i + D));
+        Sel<NV> sel;
+        make_sel(sel, y);
+        const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
+#pragma unroll
+        for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
+      }
     }
     uint8_t *out = a.out + s * a.out_stripe_stride + off;
 #pragma unroll
@@ -527,13 +532,20 @@ KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_
       {"decode_matrix_e8_nv1", "decode_matrix_e8_nv2", "decode_matrix_e8_nv4"}};
   const int nv = std::min(env_nv(4), max_nv);
   const int ni = nv == 1 ? 0 : nv == 2 ? 1 : 2;
-  return {Variant::kMatrix, static_cast<int>(n_out), nv, kNames[n_out][ni]};
+  KernelChoice kc{Variant::kMatrix, static_cast<int>(n_out), nv, kNames[n_out][ni]};
+  const char *pf = getenv("RS_AMD_PREFETCH");  // inputs in flight per lane (1, 2, 4)
+  kc.prefetch = pf ? atoi(pf) : 2;
+  return kc;
 }
 
-#define RS_MAT_CASE(E_, NV_)                                                     \
-  if (kc.size == E_ && kc.nv == NV_) {                                           \
-    hipLaunchKernelGGL((k_decode_matrix<E_, NV_>), grid, dim3(kBlock), 0, s, a); \
-    return hipGetLastError();                                                    \
+#define RS_MAT_CASE(E_, NV_)                                                                  \
+  if (kc.size == E_ && kc.nv == NV_) {                                                        \
+    switch (kc.prefetch) {                                                                    \
+      case 1: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 1>), grid, dim3(kBlock), 0, s, a); break; \
+      case 4: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 4>), grid, dim3(kBlock), 0, s, a); break; \
+      default: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 2>), grid, dim3(kBlock), 0, s, a); break; \
+    }                                                                                         \
+    return hipGetLastError();                                                                 \
   }
 #define RS_MAT_NV(E_) RS_MAT_CASE(E_, 1) RS_MAT_CASE(E_, 2) RS_MAT_CASE(E_, 4)
 

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--nv", type=str, default="1,2,4")
     ap.add_argument("--decode", type=str, default="", help="comma list of RS_AMD_DECODE values")
+    ap.add_argument("--var", action="append", default=[], help="NAME=v1,v2: extra env var to sweep")
     args = ap.parse_args()
     k, m, sb, n = args.k, args.m, args.shard_bytes, args.stripes
     erase = [int(x) for x in args.erase.split(",") if x]
@@ -41,7 +42,9 @@ def main():
     restored = torch.empty((n, max(e, 1), sb), dtype=torch.uint8, device=dev)
     nvs = [x for x in args.nv.split(",") if x]
     decs = [x for x in args.decode.split(",") if x] or [""]
-    variants = list(itertools.product(nvs, decs))
+    extra = [(kv.split("=", 1)[0], kv.split("=", 1)[1].split(",")) for kv in args.var]
+    variants = [tuple(v[:2]) + (tuple(zip([e[0] for e in extra], v[2:])),)
+                for v in itertools.product(nvs, decs, *[e[1] for e in extra])]
     res = {v: {"enc": [], "rec": []} for v in variants}
     s = torch.cuda.current_stream()
 
@@ -57,6 +60,8 @@ def main():
     ref = None
     for r in range(args.rounds + 1):
         for v in variants:
+            for name, val in v[2]:
+                os.environ[name] = val
             os.environ["RS_AMD_NV"] = v[0]
             if v[1]:
                 os.environ["RS_AMD_DECODE"] = v[1]
@@ -79,11 +84,13 @@ def main():
     for v in variants:
         te, tr = float(np.median(res[v]["enc"])), float(np.median(res[v]["rec"]))
         os.environ["RS_AMD_NV"] = v[0]
+        for name, val in v[2]:
+            os.environ[name] = val
         if v[1]:
             os.environ["RS_AMD_DECODE"] = v[1]
         else:
             os.environ.pop("RS_AMD_DECODE", None)
-        row = {"nv": v[0], "decode": v[1] or "default",
+        row = {"nv": v[0], "decode": v[1] or "default", **{n: val for n, val in v[2]},
                "enc_kernel": R.encode_kernel_name(k, m, sb), "rec_kernel": R.reconstruct_kernel_name(k, m, sb, present),
                "enc_ms": round(te, 3), "enc_TBps": round(enc_bytes / te / 1e9, 3),
                "rec_ms": round(tr, 3), "rec_TBps": round(rec_bytes / tr / 1e9, 3),
