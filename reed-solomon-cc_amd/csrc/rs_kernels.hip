@@ -202,23 +202,36 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     Sym<NV> acc[E];
 #pragma unroll
     for (int j = 0; j < E; j++) dev::zero(acc[j]);
-    // prefetch ring: inputs i..i+D-1 in flight while input i is multiplied
-    Sym<NV> buf[D];
-#pragma unroll
-    for (int d = 0; d < D; d++)
-      if (static_cast<uint32_t>(d) < n_in) dev::load_sym(buf[d], in_ptr(d));
-    for (uint32_t i0 = 0; i0 < n_in; i0 += D) {
-#pragma unroll
-      for (int d = 0; d < D; d++) {
-        const uint32_t i = i0 + d;
-        if (i >= n_in) break;
-        const Sym<NV> y = buf[d];
-        if (i + D < n_in) dev::load_sym(buf[d], in_ptr(i + D));
+    if constexpr (D == 1) {
+      // one input ahead: input i+1 in flight while input i is multiplied
+      Sym<NV> y;
+      dev::load_sym(y, in_ptr(0));
+      for (uint32_t i = 0; i < n_in; i++) {
+        Sym<NV> nxt = y;
+        if (i + 1 < n_in) dev::load_sym(nxt, in_ptr(i + 1));
         Sel<NV> sel;
         make_sel(sel, y);
         const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
 #pragma unroll
         for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
+        y = nxt;
+      }
+    } else {
+      // batches of D inputs: D loads in flight together, then D x E MACs
+      for (uint32_t i0 = 0; i0 < n_in; i0 += D) {
+        Sym<NV> y[D];
+#pragma unroll
+        for (int d = 0; d < D; d++)
+          if (i0 + d < n_in) dev::load_sym(y[d], in_ptr(i0 + d));
+#pragma unroll
+        for (int d = 0; d < D; d++) {
+          if (i0 + d >= n_in) break;
+          Sel<NV> sel;
+          make_sel(sel, y[d]);
+          const RsTab *row = a.tab_mat + static_cast<uint64_t>(i0 + d) * E;
+#pragma unroll
+          for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
+        }
       }
     }
     uint8_t *out = a.out + s * a.out_stripe_stride + off;
@@ -534,16 +547,17 @@ KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_
   const int ni = nv == 1 ? 0 : nv == 2 ? 1 : 2;
   KernelChoice kc{Variant::kMatrix, static_cast<int>(n_out), nv, kNames[n_out][ni]};
   const char *pf = getenv("RS_AMD_PREFETCH");  // inputs in flight per lane (1, 2, 4)
-  kc.prefetch = pf ? atoi(pf) : 2;
+  kc.prefetch = pf ? atoi(pf) : 1;
   return kc;
 }
 
 #define RS_MAT_CASE(E_, NV_)                                                                  \
   if (kc.size == E_ && kc.nv == NV_) {                                                        \
     switch (kc.prefetch) {                                                                    \
-      case 1: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 1>), grid, dim3(kBlock), 0, s, a); break; \
+      case 2: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 2>), grid, dim3(kBlock), 0, s, a); break; \
       case 4: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 4>), grid, dim3(kBlock), 0, s, a); break; \
-      default: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 2>), grid, dim3(kBlock), 0, s, a); break; \
+      case 5: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 5>), grid, dim3(kBlock), 0, s, a); break; \
+      default: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 1>), grid, dim3(kBlock), 0, s, a); break; \
     }                                                                                         \
     return hipGetLastError();                                                                 \
   }
