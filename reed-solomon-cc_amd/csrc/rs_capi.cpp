@@ -430,6 +430,7 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
   a.k = static_cast<uint32_t>(k);
   a.tabs_per_chunk = plan->tabs_per_chunk;
   a.work = plan->work;
+  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
   if (kc.variant == Variant::kRegister) {
     a.n_stripes = n_stripes;
     HIP_TRY(launch_encode(kc, a, s));
@@ -505,6 +506,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   a.tab_mat = reinterpret_cast<const RsTab *>(base + plan->off_mat);
   a.n_in = plan->n_in;
   a.n_out = plan->e;
+  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
   if (!a.orig) a.orig = a.rec;  // never dereferenced for absent shards
   if (!a.rec) a.rec = a.orig;
   if (kc.variant != Variant::kGeneric) {

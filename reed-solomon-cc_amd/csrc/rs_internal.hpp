@@ -29,6 +29,7 @@ struct EncodeArgs {
   uint32_t work;            // Wenc = alignUp(k, chunk) (generic path scratch positions)
   uint8_t *scratch;      // generic path only: [stripe][Wenc][sb]
   uint64_t scratch_stripes;
+  bool contig;           // lane layout (dev::load_sym): contiguous waves vs split halves
 };
 
 // Reconstruct: positions per root.zig:199-229 (recovery at [0,m), originals at
@@ -61,6 +62,7 @@ struct DecodeArgs {
   const RsTab *tab_mat;
   uint32_t n_in;
   uint32_t n_out;
+  bool contig;  // lane layout (dev::load_sym)
 };
 constexpr int32_t kSrcRecovery = 0x40000000;
 constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
@@ -86,6 +88,9 @@ constexpr uint32_t kMatrixMaxOut = 8;
 
 hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
 hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s);
+
+// contiguous lane layout possible for this shard size and lane width?
+inline bool contig_ok(uint64_t shard_bytes, int nv) { return shard_bytes % (512ull * nv) == 0; }
 
 // Engine shims (generic, in place on a single-stripe work buffer)
 hipError_t launch_engine_fft(uint8_t *work, uint64_t shard_bytes, uint64_t pos, uint64_t size, uint64_t trunc,

@@ -39,21 +39,13 @@ __host__ __device__ constexpr int ifft_tabs_ce(int size) {
   return n + (d < size ? 1 : 0);
 }
 
-// byte offset of this lane's data inside a shard (see dev::load_sym); false if
-// out of range. NV = 4 uses the contiguous 2 KiB-per-wave layout and needs
-// shard_bytes % 2048 == 0 (whole waves in range: the permlane swap needs all 64 lanes).
+// byte offset of this lane's data inside a shard (dev::lane_byte_offset); false
+// if the lane's unit is past the shard end (whole waves, see the layouts).
 template <int NV>
-__device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, uint64_t &off) {
-  constexpr uint32_t kUnitsPerChunk = 8 / NV;
+__device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, bool contig, uint64_t &off) {
   const uint64_t unit = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  const uint64_t units = shard_bytes / 64 * kUnitsPerChunk;
-  if (unit >= units) return false;
-  if constexpr (NV == 4) {
-    const uint64_t lane = unit % 64;
-    off = unit / 64 * 2048 + (lane % 32) / 2 * 64 + (lane >= 32 ? 32 : 0) + (lane % 2) * 16;
-  } else {
-    off = unit / kUnitsPerChunk * 64 + unit % kUnitsPerChunk * (4 * NV);
-  }
+  if (unit >= shard_bytes / 64 * (8 / NV)) return false;
+  off = dev::lane_byte_offset<NV>(unit / 64, static_cast<uint32_t>(unit % 64), contig);
   return true;
 }
 
@@ -61,7 +53,7 @@ __device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, uint64_t &off)
 template <int C, int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
   uint64_t off;
-  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   constexpr int TI = ifft_tabs_ce(C);
   const uint64_t sb = a.shard_bytes;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
@@ -70,7 +62,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
     // first chunk: root.zig:143-146
 #pragma unroll
     for (int p = 0; p < C; p++) {
-      if (static_cast<uint32_t>(p) < a.trunc_first) dev::load_sym(acc[p], src + p * sb);
+      if (static_cast<uint32_t>(p) < a.trunc_first) dev::load_sym(acc[p], src + p * sb, a.contig);
       else dev::zero(acc[p]);
     }
     dev::ifft_regs<C>(acc, a.tabs, a.trunc_first);
@@ -81,7 +73,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
       Sym<NV> cur[C];
 #pragma unroll
       for (int p = 0; p < C; p++) {
-        if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb);
+        if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb, a.contig);
         else dev::zero(cur[p]);
       }
       dev::ifft_regs<C>(cur, a.tabs + j * TI, t);
@@ -93,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
     uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
 #pragma unroll
     for (int p = 0; p < C; p++)
-      if (static_cast<uint32_t>(p) < a.m) dev::store_sym(dst + p * sb, acc[p]);
+      if (static_cast<uint32_t>(p) < a.m) dev::store_sym(dst + p * sb, acc[p], a.contig);
   }
 }
 
@@ -112,7 +104,7 @@ __device__ __forceinline__ void derivative_regs(Sym<NV> *w) {
 template <int W, int NV>
 __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
   uint64_t off;
-  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
@@ -124,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
       const int32_t src = ((const __attribute__((address_space(4))) int32_t *)a.pos_src)[p];
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
+        dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, a.contig);
         dev::mul_inplace(w[p], dev::load_tab(a.tab_pre + p));
       } else {
         dev::zero(w[p]);
@@ -139,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
       const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)a.pos_dst)[p];
       if (dst >= 0) {
         dev::mul_inplace(w[p], dev::load_tab(a.tab_post + p));
-        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, w[p]);
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, w[p], a.contig);
       }
     }
   }
@@ -187,7 +179,7 @@ __device__ __forceinline__ void mac_sel(Sym<NV> &x, const Sel<NV> &s, const Tab 
 template <int E, int NV, int D>
 __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
   uint64_t off;
-  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes;
   typedef const __attribute__((address_space(4))) int32_t *CI;
   const CI srcs = (CI)(a.pos_src);
@@ -205,10 +197,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     if constexpr (D == 1) {
       // one input ahead: input i+1 in flight while input i is multiplied
       Sym<NV> y;
-      dev::load_sym(y, in_ptr(0));
+      dev::load_sym(y, in_ptr(0), a.contig);
       for (uint32_t i = 0; i < n_in; i++) {
         Sym<NV> nxt = y;
-        if (i + 1 < n_in) dev::load_sym(nxt, in_ptr(i + 1));
+        if (i + 1 < n_in) dev::load_sym(nxt, in_ptr(i + 1), a.contig);
         Sel<NV> sel;
         make_sel(sel, y);
         const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
@@ -222,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
         Sym<NV> y[D];
 #pragma unroll
         for (int d = 0; d < D; d++)
-          if (i0 + d < n_in) dev::load_sym(y[d], in_ptr(i0 + d));
+          if (i0 + d < n_in) dev::load_sym(y[d], in_ptr(i0 + d), a.contig);
 #pragma unroll
         for (int d = 0; d < D; d++) {
           if (i0 + d >= n_in) break;
@@ -236,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     }
     uint8_t *out = a.out + s * a.out_stripe_stride + off;
 #pragma unroll
-    for (int j = 0; j < E; j++) dev::store_sym(out + static_cast<uint64_t>(j) * sb, acc[j]);
+    for (int j = 0; j < E; j++) dev::store_sym(out + static_cast<uint64_t>(j) * sb, acc[j], a.contig);
   }
 }
 
@@ -370,7 +362,7 @@ __device__ __forceinline__ void xor_mem(uint8_t *a, const uint8_t *b) {
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
   uint64_t off;
-  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes, C = a.chunk;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
     const uint8_t *src = a.data + s * a.data_stripe_stride + off;
@@ -392,7 +384,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
     for (uint64_t p = 0; p < a.m; p++) {
       Sym<NV> v;
       ld(v, work + p * sb);
-      dev::store_sym(dst + p * sb, v);
+      dev::store_sym(dst + p * sb, v, a.contig);
     }
   }
 }
@@ -400,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
   uint64_t off;
-  if (!lane_offset<NV>(a.shard_bytes, off)) return;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes, W = a.work;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
@@ -411,7 +403,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
       Sym<NV> v;
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb);
+        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, a.contig);
         dev::mul_inplace(v, dev::load_tab(a.tab_pre + p));
       } else {
         dev::zero(v);
@@ -431,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
         Sym<NV> v;
         ld(v, work + p * sb);
         dev::mul_inplace(v, dev::load_tab(a.tab_post + p));
-        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, v);
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, v, a.contig);
       }
     }
   }
@@ -441,14 +433,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
 __global__ __launch_bounds__(kBlock) void k_engine_transform(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size,
                                                              uint64_t trunc, const RsTab *tabs, int inverse) {
   uint64_t off;
-  if (!lane_offset<1>(sb, off)) return;
+  if (!lane_offset<1>(sb, false, off)) return;
   if (inverse) ifft_mem<1>(work + off, sb, pos, size, trunc, tabs);
   else fft_mem<1>(work + off, sb, pos, size, trunc, tabs);
 }
 
 __global__ __launch_bounds__(kBlock) void k_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab) {
   uint64_t off;
-  if (!lane_offset<1>(bytes, off)) return;
+  if (!lane_offset<1>(bytes, false, off)) return;
   Sym<1> v;
   ld(v, chunks + off);
   dev::mul_inplace(v, dev::load_tab(tab));
@@ -503,14 +495,9 @@ static const char *reg_name(bool enc, int size, int nv) {
   return enc ? kEnc[si][ni] : kDec[si][ni];
 }
 
-// the NV = 4 lane layout covers 2 KiB per wave
-static int shard_nv(int max_nv, uint64_t shard_bytes) {
-  return (max_nv >= 4 && shard_bytes % 2048 != 0) ? 2 : max_nv;
-}
-
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
   (void)k;
-  max_nv = shard_nv(max_nv, shard_bytes);
+  (void)shard_bytes;
   const uint64_t C = ceil_pow2(m);
   if (C <= 16) {
     const int c = static_cast<int>(C);
@@ -521,7 +508,7 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
 }
 
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
-  max_nv = shard_nv(max_nv, shard_bytes);
+  (void)shard_bytes;
   const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
   if (W <= 32) {
     const int w = static_cast<int>(W);
@@ -532,7 +519,7 @@ KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
 }
 
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv) {
-  max_nv = shard_nv(max_nv, shard_bytes);
+  (void)shard_bytes;
   static const char *kNames[9][3] = {
       {"", "", ""},
       {"decode_matrix_e1_nv1", "decode_matrix_e1_nv2", "decode_matrix_e1_nv4"},
