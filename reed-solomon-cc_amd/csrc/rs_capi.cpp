@@ -431,7 +431,7 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
   a.tabs_per_chunk = plan->tabs_per_chunk;
   a.work = plan->work;
   a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
-  if (kc.variant == Variant::kRegister) {
+  if (kc.variant != Variant::kGeneric) {
     a.n_stripes = n_stripes;
     HIP_TRY(launch_encode(kc, a, s));
     return RS_OK;

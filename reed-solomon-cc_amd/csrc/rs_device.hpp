@@ -205,9 +205,12 @@ struct VecT<4> {
 //             the matching hi pieces; one v_permlane32_swap per dword then pairs every
 //             lane's lo with its hi. p = the lane's first address, second at p + 64*P.
 // Measured on MI355X (tools/hbm_probe.hip): contiguous wave accesses stream ~5% faster.
+// `base` is wave-uniform (stripe/shard start) and `off` the lane's 32-bit offset,
+// so the compiler can use the SGPR-base form of global_load/store (saddr + voffset).
 template <int NV>
-__device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__ p, bool contig) {
+__device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__ base, uint32_t off, bool contig) {
   typedef typename VecT<NV>::type V;
+  const uint8_t *p = base + off;
   const V a = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
   const V b = __builtin_nontemporal_load(reinterpret_cast<const V *>(p + (contig ? 256 * NV : 32)));
   if constexpr (NV == 1) {
@@ -231,8 +234,9 @@ __device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__
 }
 
 template <int NV>
-__device__ __forceinline__ void store_sym(uint8_t *__restrict__ p, const Sym<NV> &s, bool contig) {
+__device__ __forceinline__ void store_sym(uint8_t *__restrict__ base, uint32_t off, const Sym<NV> &s, bool contig) {
   typedef typename VecT<NV>::type V;
+  uint8_t *p = base + off;
   uint32_t l[NV], h[NV];
 #pragma unroll
   for (int v = 0; v < NV; v++) {
@@ -266,14 +270,15 @@ __device__ __forceinline__ void store_sym(uint8_t *__restrict__ p, const Sym<NV>
 // the layouts above. contig needs shard_bytes % (512*NV) == 0 so every wave is
 // whole (the swap needs all 64 lanes).
 template <int NV>
-__device__ __forceinline__ uint64_t lane_byte_offset(uint64_t wave, uint32_t lane, bool contig) {
+__device__ __forceinline__ uint32_t lane_byte_offset(uint64_t wave, uint32_t lane, bool contig) {
   constexpr uint32_t P = 4 * NV, kPiecesPerHalf = 32 / P;
   if (contig) {
     const uint32_t ll = lane % 32;
-    return wave * (128 * P) + ll / kPiecesPerHalf * 64 + (lane >= 32 ? 32 : 0) + ll % kPiecesPerHalf * P;
+    return static_cast<uint32_t>(wave * (128 * P) + ll / kPiecesPerHalf * 64 + (lane >= 32 ? 32 : 0) +
+                                 ll % kPiecesPerHalf * P);
   }
   const uint64_t unit = wave * 64 + lane;
-  return unit / (8 / NV) * 64 + unit % (8 / NV) * P;
+  return static_cast<uint32_t>(unit / (8 / NV) * 64 + unit % (8 / NV) * P);
 }
 
 }  // namespace dev

@@ -69,7 +69,7 @@ constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
 
 // Kernel variants: fused register-resident for small transforms, generic
 // (per-lane column walk over an HBM scratch work buffer) otherwise.
-enum class Variant { kRegister, kGeneric, kMatrix };
+enum class Variant { kRegister, kGeneric, kMatrix, kWaveSplit };
 
 struct KernelChoice {
   Variant variant;

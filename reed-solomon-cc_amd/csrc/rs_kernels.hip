@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "rs_device.hpp"
 #include "rs_internal.hpp"
@@ -42,7 +43,7 @@ __host__ __device__ constexpr int ifft_tabs_ce(int size) {
 // byte offset of this lane's data inside a shard (dev::lane_byte_offset); false
 // if the lane's unit is past the shard end (whole waves, see the layouts).
 template <int NV>
-__device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, bool contig, uint64_t &off) {
+__device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, bool contig, uint32_t &off) {
   const uint64_t unit = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   if (unit >= shard_bytes / 64 * (8 / NV)) return false;
   off = dev::lane_byte_offset<NV>(unit / 64, static_cast<uint32_t>(unit % 64), contig);
@@ -52,17 +53,17 @@ __device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, bool contig, u
 // ============================================================ fused encode
 template <int C, int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   constexpr int TI = ifft_tabs_ce(C);
   const uint64_t sb = a.shard_bytes;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    const uint8_t *src = a.data + s * a.data_stripe_stride + off;
+    const uint8_t *src = a.data + s * a.data_stripe_stride;
     Sym<NV> acc[C];
     // first chunk: root.zig:143-146
 #pragma unroll
     for (int p = 0; p < C; p++) {
-      if (static_cast<uint32_t>(p) < a.trunc_first) dev::load_sym(acc[p], src + p * sb, a.contig);
+      if (static_cast<uint32_t>(p) < a.trunc_first) dev::load_sym(acc[p], src + p * sb, off, a.contig);
       else dev::zero(acc[p]);
     }
     dev::ifft_regs<C>(acc, a.tabs, a.trunc_first);
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
       Sym<NV> cur[C];
 #pragma unroll
       for (int p = 0; p < C; p++) {
-        if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb, a.contig);
+        if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb, off, a.contig);
         else dev::zero(cur[p]);
       }
       dev::ifft_regs<C>(cur, a.tabs + j * TI, t);
@@ -82,10 +83,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
     }
     // root.zig:169
     dev::fft_regs<C>(acc, a.tabs + a.n_chunks * TI, a.m);
-    uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride;
 #pragma unroll
     for (int p = 0; p < C; p++)
-      if (static_cast<uint32_t>(p) < a.m) dev::store_sym(dst + p * sb, acc[p], a.contig);
+      if (static_cast<uint32_t>(p) < a.m) dev::store_sym(dst + p * sb, off, acc[p], a.contig);
   }
 }
 
@@ -103,12 +104,12 @@ __device__ __forceinline__ void derivative_regs(Sym<NV> *w) {
 
 template <int W, int NV>
 __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
-    const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+    const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
+    const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
     Sym<NV> w[W];
     // erasure masks on received shards, zero elsewhere: root.zig:291-303
 #pragma unroll
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
       const int32_t src = ((const __attribute__((address_space(4))) int32_t *)a.pos_src)[p];
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, a.contig);
+        dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, off, a.contig);
         dev::mul_inplace(w[p], dev::load_tab(a.tab_pre + p));
       } else {
         dev::zero(w[p]);
@@ -125,14 +126,139 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
     dev::ifft_regs<W>(w, a.tab_ifft, a.trunc);  // root.zig:306
     derivative_regs<W>(w);                      // root.zig:309-315
     dev::fft_regs<W>(w, a.tab_fft, a.trunc);    // root.zig:318
-    uint8_t *out = a.out + s * a.out_stripe_stride + off;
+    uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
     for (int p = 0; p < W; p++) {  // root.zig:321-326
       const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)a.pos_dst)[p];
       if (dst >= 0) {
         dev::mul_inplace(w[p], dev::load_tab(a.tab_post + p));
-        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, w[p], a.contig);
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, off, w[p], a.contig);
       }
+    }
+  }
+}
+
+// ============================================ wave-split encode, chunk = 64
+// For m in 33..64 the 64-point chunk transforms do not fit one lane's VGPRs.
+// Four waves share the SAME 64 column units (lanes) and split the positions:
+// layout A — wave w holds positions 16w+j (radix-4 stages on bits (0,1), (2,3)
+// are wave-local); layout B — wave w holds positions i + 4w + 16q (stage on
+// bits (4,5) wave-local). A <-> B is one LDS transpose per chunk. Every twiddle
+// a wave needs is still wave-uniform (its group base depends only on w), so
+// tables stay in SGPRs. Mirrors Encoder.encode (root.zig:136-173).
+template <int NV>
+struct LdsSym {
+  uint32_t v[2 * NV];
+};
+
+template <int NV>
+__device__ __forceinline__ void lds_put(LdsSym<NV> *row, uint32_t lane, const Sym<NV> &x) {
+  LdsSym<NV> t;
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    t.v[2 * v] = x.l[v];
+    t.v[2 * v + 1] = x.h[v];
+  }
+  row[lane] = t;
+}
+
+template <int NV>
+__device__ __forceinline__ void lds_get(const LdsSym<NV> *row, uint32_t lane, Sym<NV> &x) {
+  const LdsSym<NV> t = row[lane];
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    x.l[v] = t.v[2 * v];
+    x.h[v] = t.v[2 * v + 1];
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void ifft4(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<NV> &s3, const RsTab *g) {
+  const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+  dev::ifft_bf(s0, s1, m01);
+  dev::ifft_bf(s2, s3, m23);
+  dev::ifft_bf(s0, s2, m02);
+  dev::ifft_bf(s1, s3, m02);
+}
+
+template <int NV>
+__device__ __forceinline__ void fft4(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<NV> &s3, const RsTab *g) {
+  const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+  dev::fft_bf(s0, s2, m02);
+  dev::fft_bf(s1, s3, m02);
+  dev::fft_bf(s0, s1, m01);
+  dev::fft_bf(s2, s3, m23);
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
+  constexpr int TI = 63;  // ifft_tab_count(64): 16 + 4 + 1 groups x 3
+  __shared__ LdsSym<NV> lds[64][64];
+  const uint64_t sb = a.shard_bytes;
+  const uint64_t regions = sb / 64 * (8 / NV) / 64;
+  if (blockIdx.x >= regions) return;  // whole block: every wave shares the region
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *src = a.data + s * a.data_stripe_stride;
+    Sym<NV> acc[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) dev::zero(acc[u]);
+    for (uint32_t c = 0; c < a.n_chunks; c++) {
+      const uint32_t t = c == 0 ? a.trunc_first : (c + 1 == a.n_chunks ? a.trunc_last : 64u);
+      const RsTab *tc = a.tabs + c * TI;
+      Sym<NV> cur[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {  // layout A
+        const uint32_t pos = 16 * w + j;
+        if (pos < t) dev::load_sym(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
+        else dev::zero(cur[j]);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; g++) {  // stage d=1, groups r = 16w + 4g
+        const uint32_t r = 16 * w + 4 * g;
+        if (r < t) ifft4(cur[4 * g], cur[4 * g + 1], cur[4 * g + 2], cur[4 * g + 3], tc + r / 4 * 3);
+      }
+      if (16 * w < t) {  // stage d=4, group r = 16w
+#pragma unroll
+        for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 48 + w * 3);
+      }
+      __syncthreads();  // previous readers of lds are done
+#pragma unroll
+      for (int j = 0; j < 16; j++) lds_put(lds[16 * w + j], lane, cur[j]);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 16; u++) lds_get(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, cur[u]);  // layout B
+#pragma unroll
+      for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 60);  // d=16
+#pragma unroll
+      for (int u = 0; u < 16; u++) dev::xor_into(acc[u], cur[u]);  // root.zig:153-155
+    }
+    // FFT(0, 64, trunc m) on acc, root.zig:169
+    const RsTab *tf = a.tabs + a.n_chunks * TI;
+#pragma unroll
+    for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf);  // d=16 (layout B)
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; u++) lds_put(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, acc[u]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; j++) lds_get(lds[16 * w + j], lane, acc[j]);  // layout A
+    if (16 * w < a.m) {  // d=4, group r = 16w
+#pragma unroll
+      for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf + 3 + w * 3);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; g++) {  // d=1, groups r = 16w + 4g
+      const uint32_t r = 16 * w + 4 * g;
+      if (r < a.m) fft4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3], tf + 15 + r / 4 * 3);
+    }
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t pos = 16 * w + j;
+      if (pos < a.m) dev::store_sym(dst + pos * sb, off, acc[j], a.contig);
     }
   }
 }
@@ -178,15 +304,15 @@ __device__ __forceinline__ void mac_sel(Sym<NV> &x, const Sel<NV> &s, const Tab 
 
 template <int E, int NV, int D>
 __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes;
   typedef const __attribute__((address_space(4))) int32_t *CI;
   const CI srcs = (CI)(a.pos_src);
   const uint32_t n_in = a.n_in;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
-    const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+    const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
+    const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
     auto in_ptr = [&](uint32_t i) {
       const int32_t src = srcs[i];
       return ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb;
@@ -197,10 +323,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     if constexpr (D == 1) {
       // one input ahead: input i+1 in flight while input i is multiplied
       Sym<NV> y;
-      dev::load_sym(y, in_ptr(0), a.contig);
+      dev::load_sym(y, in_ptr(0), off, a.contig);
       for (uint32_t i = 0; i < n_in; i++) {
         Sym<NV> nxt = y;
-        if (i + 1 < n_in) dev::load_sym(nxt, in_ptr(i + 1), a.contig);
+        if (i + 1 < n_in) dev::load_sym(nxt, in_ptr(i + 1), off, a.contig);
         Sel<NV> sel;
         make_sel(sel, y);
         const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
@@ -214,7 +340,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
         Sym<NV> y[D];
 #pragma unroll
         for (int d = 0; d < D; d++)
-          if (i0 + d < n_in) dev::load_sym(y[d], in_ptr(i0 + d), a.contig);
+          if (i0 + d < n_in) dev::load_sym(y[d], in_ptr(i0 + d), off, a.contig);
 #pragma unroll
         for (int d = 0; d < D; d++) {
           if (i0 + d >= n_in) break;
@@ -226,9 +352,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
         }
       }
     }
-    uint8_t *out = a.out + s * a.out_stripe_stride + off;
+    uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
-    for (int j = 0; j < E; j++) dev::store_sym(out + static_cast<uint64_t>(j) * sb, acc[j], a.contig);
+    for (int j = 0; j < E; j++) dev::store_sym(out + static_cast<uint64_t>(j) * sb, off, acc[j], a.contig);
   }
 }
 
@@ -361,7 +487,7 @@ __device__ __forceinline__ void xor_mem(uint8_t *a, const uint8_t *b) {
 
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes, C = a.chunk;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
@@ -384,14 +510,14 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
     for (uint64_t p = 0; p < a.m; p++) {
       Sym<NV> v;
       ld(v, work + p * sb);
-      dev::store_sym(dst + p * sb, v, a.contig);
+      dev::store_sym(dst + p * sb, 0u, v, a.contig);
     }
   }
 }
 
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes, W = a.work;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
@@ -403,7 +529,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
       Sym<NV> v;
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, a.contig);
+        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, a.contig);
         dev::mul_inplace(v, dev::load_tab(a.tab_pre + p));
       } else {
         dev::zero(v);
@@ -423,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
         Sym<NV> v;
         ld(v, work + p * sb);
         dev::mul_inplace(v, dev::load_tab(a.tab_post + p));
-        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, v, a.contig);
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, 0u, v, a.contig);
       }
     }
   }
@@ -432,14 +558,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
 // ========================================================== engine test shims
 __global__ __launch_bounds__(kBlock) void k_engine_transform(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size,
                                                              uint64_t trunc, const RsTab *tabs, int inverse) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<1>(sb, false, off)) return;
   if (inverse) ifft_mem<1>(work + off, sb, pos, size, trunc, tabs);
   else fft_mem<1>(work + off, sb, pos, size, trunc, tabs);
 }
 
 __global__ __launch_bounds__(kBlock) void k_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab) {
-  uint64_t off;
+  uint32_t off;
   if (!lane_offset<1>(bytes, false, off)) return;
   Sym<1> v;
   ld(v, chunks + off);
@@ -466,6 +592,8 @@ static int clamp_nv(int nv, int size, bool enc) {
   while (nv > 1 && live * 2 * nv > limit) nv >>= 1;
   return nv;
 }
+
+static const char *env_variant() { return getenv("RS_AMD_VARIANT"); }
 
 static int env_nv(int dflt) {
   const char *e = getenv("RS_AMD_NV");
@@ -503,6 +631,11 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
     const int c = static_cast<int>(C);
     const int nv = clamp_nv(std::min(env_nv(4), max_nv), c, true);
     return {Variant::kRegister, c, nv, reg_name(true, c, nv)};
+  }
+  if (C == 64 && shard_bytes % 512 == 0 && (env_variant() == nullptr || std::string(env_variant()) != "generic")) {
+    int nv = std::min(std::min(env_nv(1), max_nv), 2);
+    if (shard_bytes % (512 * nv)) nv = 1;  // whole 64-lane regions only
+    return {Variant::kWaveSplit, 64, nv, nv == 1 ? "encode_ws64_nv1" : "encode_ws64_nv2"};
   }
   return {Variant::kGeneric, static_cast<int>(C), 1, "encode_generic_nv1"};
 }
@@ -571,6 +704,14 @@ hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_
     RS_ENC_CASE(8, 1) RS_ENC_CASE(8, 2)
     RS_ENC_CASE(16, 1)
     return hipErrorInvalidValue;
+  }
+  if (kc.variant == Variant::kWaveSplit) {
+    // one block per 64-lane region; 4 waves split the 64 positions
+    const uint64_t regions = a.shard_bytes / 64 * (8 / kc.nv) / 64;
+    const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
+    if (kc.nv == 1) hipLaunchKernelGGL(k_encode_ws64<1>, g, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(k_encode_ws64<2>, g, dim3(kBlock), 0, s, a);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL(k_encode_generic<1>, grid, dim3(kBlock), 0, s, a);
   return hipGetLastError();
