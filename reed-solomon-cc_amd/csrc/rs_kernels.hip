@@ -57,7 +57,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   constexpr int TI = ifft_tabs_ce(C);
   const uint64_t sb = a.shard_bytes;
-  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+  {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
+    const uint64_t s = blockIdx.y;
     const uint8_t *src = a.data + s * a.data_stripe_stride;
     Sym<NV> acc[C];
     // first chunk: root.zig:143-146
@@ -77,7 +78,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
         if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb, off, a.contig);
         else dev::zero(cur[p]);
       }
-      dev::ifft_regs<C>(cur, a.tabs + j * TI, t);
+      const RsTab *tj = a.tabs + j * TI;
+      asm volatile("" : "+s"(tj));  // opaque base: no per-group pointer IVs (SGPR spills)
+      dev::ifft_regs<C>(cur, tj, t);
 #pragma unroll
       for (int p = 0; p < C; p++) dev::xor_into(acc[p], cur[p]);
     }
@@ -107,7 +110,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
   uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes;
-  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+  {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
+    const uint64_t s = blockIdx.y;
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
     Sym<NV> w[W];
@@ -172,22 +176,32 @@ __device__ __forceinline__ void lds_get(const LdsSym<NV> *row, uint32_t lane, Sy
   }
 }
 
+// The scheduling barriers keep the compiler from hoisting the tables of many
+// groups at once (each table is 21 SGPRs; hoisting spills SGPRs to VGPR lanes).
 template <int NV>
 __device__ __forceinline__ void ifft4(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<NV> &s3, const RsTab *g) {
-  const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+  __builtin_amdgcn_sched_barrier(0);
+  const Tab m01 = dev::load_tab(g);
   dev::ifft_bf(s0, s1, m01);
+  const Tab m23 = dev::load_tab(g + 2);
   dev::ifft_bf(s2, s3, m23);
+  const Tab m02 = dev::load_tab(g + 1);
   dev::ifft_bf(s0, s2, m02);
   dev::ifft_bf(s1, s3, m02);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int NV>
 __device__ __forceinline__ void fft4(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<NV> &s3, const RsTab *g) {
-  const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+  __builtin_amdgcn_sched_barrier(0);
+  const Tab m02 = dev::load_tab(g + 1);
   dev::fft_bf(s0, s2, m02);
   dev::fft_bf(s1, s3, m02);
+  const Tab m01 = dev::load_tab(g);
   dev::fft_bf(s0, s1, m01);
+  const Tab m23 = dev::load_tab(g + 2);
   dev::fft_bf(s2, s3, m23);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int NV>
@@ -200,7 +214,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
-  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+  {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
+    const uint64_t s = blockIdx.y;
     const uint8_t *src = a.data + s * a.data_stripe_stride;
     Sym<NV> acc[16];
 #pragma unroll
@@ -208,6 +223,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
     for (uint32_t c = 0; c < a.n_chunks; c++) {
       const uint32_t t = c == 0 ? a.trunc_first : (c + 1 == a.n_chunks ? a.trunc_last : 64u);
       const RsTab *tc = a.tabs + c * TI;
+      asm volatile("" : "+s"(tc));  // opaque base: no per-group pointer IVs (SGPR spills)
       Sym<NV> cur[16];
 #pragma unroll
       for (int j = 0; j < 16; j++) {  // layout A
@@ -310,7 +326,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
   typedef const __attribute__((address_space(4))) int32_t *CI;
   const CI srcs = (CI)(a.pos_src);
   const uint32_t n_in = a.n_in;
-  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+  {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
+    const uint64_t s = blockIdx.y;
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
     auto in_ptr = [&](uint32_t i) {
@@ -694,7 +711,40 @@ KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_
     return hipGetLastError();                                                 \
   }
 
+static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
+static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s);
+
+// The fused kernels map one stripe to one blockIdx.y (no stripe loop inside the
+// kernel: a loop lets the compiler hoist every per-stripe-invariant uniform value
+// into SGPRs and spill them), so batches are launched in slices of <= 65535 stripes.
 hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
+  if (kc.variant == Variant::kGeneric) return launch_encode_one(kc, a, s);
+  for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {
+    EncodeArgs b = a;
+    b.data += s0 * a.data_stripe_stride;
+    b.parity += s0 * a.parity_stripe_stride;
+    b.n_stripes = std::min<uint64_t>(65535, a.n_stripes - s0);
+    hipError_t e = launch_encode_one(kc, b, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
+  if (kc.variant == Variant::kGeneric) return launch_decode_one(kc, a, s);
+  for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {
+    DecodeArgs b = a;
+    b.orig += s0 * a.orig_stripe_stride;
+    b.rec += s0 * a.rec_stripe_stride;
+    b.out += s0 * a.out_stripe_stride;
+    b.n_stripes = std::min<uint64_t>(65535, a.n_stripes - s0);
+    hipError_t e = launch_decode_one(kc, b, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
   const dim3 grid = grid_for(a.shard_bytes, kc.nv, a.n_stripes);
   if (kc.variant == Variant::kRegister) {
     // live slots 2*C: NV <= 128 / (4*C)
@@ -717,7 +767,7 @@ hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
+static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
   const dim3 grid = grid_for(a.shard_bytes, kc.nv, a.n_stripes);
   if (kc.variant == Variant::kRegister) {
     // live slots W: NV <= 128 / (2*W)
