@@ -126,6 +126,22 @@ int rs_reconstruct_batch_dev(uint64_t original_count, uint64_t recovery_count, s
                              uint64_t recovery_stripe_stride, void *d_restored, uint64_t restored_stripe_stride,
                              uint32_t flags, rs_stream_t stream);
 
+/* -------------------------------------- host-resident batches (end to end)
+ * Same layouts and semantics as the *_dev calls, but the batch lives in HOST
+ * memory: the library streams it through HBM in slices with a 3-deep
+ * H2D -> kernel -> D2H pipeline on its own streams (PCIe full duplex overlapped
+ * with compute) and returns when the results are in host memory. Pinned host
+ * buffers (hipHostMalloc / hipHostRegister / torch pin_memory) run at PCIe rate;
+ * pageable buffers work but are copied through the HIP runtime's staging path. */
+int rs_encode_batch_host(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, uint64_t n_stripes,
+                         const void *h_original, uint64_t original_stripe_stride, void *h_recovery,
+                         uint64_t recovery_stripe_stride, uint32_t flags);
+int rs_reconstruct_batch_host(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                              uint64_t n_stripes, const uint8_t *present, const void *h_original,
+                              uint64_t original_stripe_stride, const void *h_recovery,
+                              uint64_t recovery_stripe_stride, void *h_restored, uint64_t restored_stripe_stride,
+                              uint32_t flags);
+
 /* Which device kernel a call would run on ("encode_reg_w4_nv4", "decode_matrix_e4_nv4",
  * "encode_generic_nv1", ...), assuming 16-byte aligned buffers. present: k+m flags as
  * for rs_reconstruct_batch_dev, or NULL for "the first min(k, m) originals lost". */

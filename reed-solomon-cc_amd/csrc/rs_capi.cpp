@@ -535,6 +535,121 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   return RS_OK;
 }
 
+// ------------------------------------------------------- host-resident batch
+namespace {
+
+// Copy `rows` rows of `row_bytes` between (possibly strided) buffers.
+hipError_t copy_rows(void *dst, uint64_t dst_stride, const void *src, uint64_t src_stride, uint64_t row_bytes,
+                     uint64_t rows, hipMemcpyKind kind, hipStream_t s) {
+  if (rows == 0 || row_bytes == 0) return hipSuccess;
+  if (dst_stride == row_bytes && src_stride == row_bytes)
+    return hipMemcpyAsync(dst, src, rows * row_bytes, kind, s);
+  return hipMemcpy2DAsync(dst, dst_stride, src, src_stride, row_bytes, rows, kind, s);
+}
+
+struct Pipeline {
+  static constexpr int kSlots = 3;
+  hipStream_t st[kSlots] = {};
+  void *buf[kSlots][3] = {};
+  ~Pipeline() {
+    for (int i = 0; i < kSlots; i++) {
+      if (st[i]) (void)hipStreamSynchronize(st[i]);
+      for (void *b : buf[i])
+        if (b) (void)hipFree(b);
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+    }
+  }
+  int init(const uint64_t bytes[3]) {
+    for (int i = 0; i < kSlots; i++) {
+      HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+      for (int j = 0; j < 3; j++)
+        if (bytes[j]) HIP_TRY(hipMalloc(&buf[i][j], bytes[j]));
+    }
+    return RS_OK;
+  }
+  int finish() {
+    for (int i = 0; i < kSlots; i++) HIP_TRY(hipStreamSynchronize(st[i]));
+    return RS_OK;
+  }
+};
+
+constexpr uint64_t kSliceBytes = 256ull << 20;  // input bytes per pipeline slice
+
+}  // namespace
+
+int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const void *h_orig, uint64_t orig_stride,
+                         void *h_rec, uint64_t rec_stride, uint32_t flags) {
+  if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  if (n == 0) return RS_OK;
+  if (!h_orig || !h_rec) return fail(RS_ERR_INVALID_ARGUMENT, "NULL host pointer");
+  if (orig_stride == 0) orig_stride = k * sb;
+  if (rec_stride == 0) rec_stride = m * sb;
+  int dev;
+  if ((st = current_device(&dev))) return st;
+  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, kSliceBytes / (k * sb)));
+  Pipeline p;
+  const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
+  if ((st = p.init(bytes))) return st;
+  for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
+    const int slot = static_cast<int>(i % Pipeline::kSlots);
+    const uint64_t cnt = std::min(S, n - s0);
+    hipStream_t q = p.st[slot];
+    HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride, orig_stride,
+                      k * sb, cnt, hipMemcpyHostToDevice, q));
+    if ((st = rs_encode_batch_dev(k, m, sb, cnt, p.buf[slot][0], 0, p.buf[slot][1], 0, flags, q))) return st;
+    HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb, m * sb,
+                      cnt, hipMemcpyDeviceToHost, q));
+  }
+  return p.finish();
+}
+
+int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const uint8_t *present,
+                              const void *h_orig, uint64_t orig_stride, const void *h_rec, uint64_t rec_stride,
+                              void *h_out, uint64_t out_stride, uint32_t flags) {
+  if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  uint64_t e = 0, have = 0;
+  for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+  for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
+  if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+  if (e == 0 || n == 0) return RS_OK;
+  if (!h_orig || !h_rec || !h_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL host pointer");
+  if (orig_stride == 0) orig_stride = k * sb;
+  if (rec_stride == 0) rec_stride = m * sb;
+  if (out_stride == 0) out_stride = e * sb;
+  int dev;
+  if ((st = current_device(&dev))) return st;
+  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, kSliceBytes / (k * sb)));
+  Pipeline p;
+  const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
+  if ((st = p.init(bytes))) return st;
+  for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
+    const int slot = static_cast<int>(i % Pipeline::kSlots);
+    const uint64_t cnt = std::min(S, n - s0);
+    hipStream_t q = p.st[slot];
+    // only the present shards cross PCIe
+    for (uint64_t j = 0; j < k; j++)
+      if (present[j])
+        HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + j * sb, k * sb,
+                          static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + j * sb, orig_stride, sb, cnt,
+                          hipMemcpyHostToDevice, q));
+    for (uint64_t j = 0; j < m; j++)
+      if (present[k + j])
+        HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + j * sb, m * sb,
+                          static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + j * sb, rec_stride, sb, cnt,
+                          hipMemcpyHostToDevice, q));
+    if ((st = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
+                                       p.buf[slot][2], 0, flags, q)))
+      return st;
+    HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb, e * sb,
+                      cnt, hipMemcpyDeviceToHost, q));
+  }
+  return p.finish();
+}
+
 // ------------------------------------------------------------ one-shot host
 namespace {
 struct DevMem {

@@ -77,6 +77,8 @@ def lib():
         "rs_decoder_free": (None, [vp]),
         "rs_encode_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32, vp]),
         "rs_reconstruct_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32, vp]),
+        "rs_encode_batch_host": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32]),
+        "rs_reconstruct_batch_host": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32]),
         "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
         "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
@@ -248,6 +250,30 @@ def reconstruct_batch_dev(original_count: int, recovery_count: int, present: Seq
         original_count, recovery_count, sb, n, pres, C.c_void_p(original.data_ptr()), original.stride(0),
         C.c_void_p(recovery.data_ptr()), recovery.stride(0), C.c_void_p(restored.data_ptr()), restored.stride(0),
         flags, _stream_handle(stream)))
+
+
+def encode_batch_host(original_count: int, recovery_count: int, data, parity, flags: int = FLAG_CORRECTED):
+    """Host-resident batch (numpy arrays or CPU tensors, ideally pinned): data [n, k, sb] -> parity [n, m, sb]."""
+    n, k, sb = data.shape
+    _check(lib().rs_encode_batch_host(original_count, recovery_count, sb, n, C.c_void_p(_host_ptr(data)), 0,
+                                      C.c_void_p(_host_ptr(parity)), 0, flags))
+
+
+def reconstruct_batch_host(original_count: int, recovery_count: int, present, original, recovery, restored,
+                           flags: int = FLAG_CORRECTED):
+    n, k, sb = original.shape
+    pres = (C.c_uint8 * (original_count + recovery_count))(*[1 if p else 0 for p in present])
+    _check(lib().rs_reconstruct_batch_host(original_count, recovery_count, sb, n, pres,
+                                           C.c_void_p(_host_ptr(original)), 0, C.c_void_p(_host_ptr(recovery)), 0,
+                                           C.c_void_p(_host_ptr(restored)), 0, flags))
+
+
+def _host_ptr(a) -> int:
+    if hasattr(a, "data_ptr"):
+        assert not a.is_cuda and a.is_contiguous()
+        return a.data_ptr()
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
 
 
 def encode_kernel_name(k, m, shard_bytes) -> str:

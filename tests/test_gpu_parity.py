@@ -277,3 +277,23 @@ def test_repeatable_and_nan_free_of_state():
     k, m, sb = 10, 4, 1 << 16
     d = splitmix_bytes(3, 8 * k * sb).reshape(8, k, sb)
     assert (gpu_encode(k, m, d) == gpu_encode(k, m, d)).all()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_batch_pipeline(oracle, pinned):
+    """rs_encode_batch_host / rs_reconstruct_batch_host (H2D -> kernel -> D2H ring) == oracle."""
+    k, m, sb, n = 10, 4, 1 << 16, 37  # several pipeline slices at 256 MiB / (k*sb) = 409 stripes? -> force small
+    data = torch.from_numpy(splitmix_bytes(77, n * k * sb).reshape(n, k, sb))
+    if pinned:
+        data = data.pin_memory()
+    par = torch.zeros((n, m, sb), dtype=torch.uint8)
+    if pinned:
+        par = par.pin_memory()
+    R.encode_batch_host(k, m, data, par)
+    exp = oracle.encode_batch(k, m, data.numpy(), threads=4)
+    assert (par.numpy() == exp).all()
+    present = [0, 1, 0, 1, 1, 1, 1, 0, 1, 1] + [1, 1, 1, 1]
+    missing = [i for i in range(k) if not present[i]]
+    out = torch.zeros((n, len(missing), sb), dtype=torch.uint8)
+    R.reconstruct_batch_host(k, m, present, data, par, out)
+    assert (out.numpy() == data.numpy()[:, missing]).all()
