@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""End-to-end (host memory in, host memory out) rate of the codec: the
+PCIe-inclusive number DESIGN.md reports beside the device-resident bench.
+
+  python tools/e2e_bench.py --stripes 1024            # RS(10,4) 1 MiB, pinned + pageable
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "reed-solomon-cc_amd"))
+import reedsol_amd as R  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--shard-bytes", type=int, default=1 << 20)
+    ap.add_argument("--stripes", type=int, default=1024)
+    ap.add_argument("--erase", type=str, default="0,1,2,3")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--pageable-stripes", type=int, default=128)
+    a = ap.parse_args()
+    k, m, sb = a.k, a.m, a.shard_bytes
+    erase = [int(x) for x in a.erase.split(",") if x]
+    present = [0 if i in erase else 1 for i in range(k)] + [1] * m
+    torch.cuda.init()
+    res = {"workload": f"RS({k},{m}) {sb} B shards", "erased": erase}
+    for mode, n in (("pinned", a.stripes), ("pageable", a.pageable_stripes)):
+        data = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8)
+        par = torch.empty((n, m, sb), dtype=torch.uint8)
+        out = torch.empty((n, len(erase), sb), dtype=torch.uint8)
+        if mode == "pinned":
+            data, par, out = data.pin_memory(), par.pin_memory(), out.pin_memory()
+        R.encode_batch_host(k, m, data[:1], par[:1])  # plan + warmup
+        R.reconstruct_batch_host(k, m, present, data[:1], par[:1], out[:1])
+        te, tr = [], []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            R.encode_batch_host(k, m, data, par)
+            te.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            R.reconstruct_batch_host(k, m, present, data, par, out)
+            tr.append(time.perf_counter() - t0)
+        ok = bool(torch.equal(out, data[:, erase]))
+        gib = k * sb * n / 2**30
+        res[mode] = {"stripes": n, "encode_GiBps": round(gib / min(te), 2),
+                     "reconstruct_GiBps": round(gib / min(tr), 2),
+                     "encode_pcie_GBps": round((k + m) * sb * n / min(te) / 1e9, 2),
+                     "reconstruct_pcie_GBps": round((k + len(erase)) * sb * n / min(tr) / 1e9, 2),
+                     "verified": ok}
+        print(json.dumps({mode: res[mode]}), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
