@@ -117,6 +117,7 @@ struct EncodePlan {
 struct DecodePlan {
   std::shared_ptr<DevBuf> buf;
   bool matrix = false;
+  bool tiled = false;
   uint32_t work = 0, chunk = 0, trunc = 0, e = 0, n_in = 0;
   size_t off_fft = 0, off_pre = 0, off_post = 0, off_src = 0, off_dst = 0, off_mat = 0;  // byte offsets into buf
 };
@@ -203,24 +204,32 @@ const char *decode_mode_env() {
 
 constexpr uint32_t flags_none() { return 0; }
 
-// Matrix kernel when it does fewer multiplies than the FFT reconstruct
-// (k*e MACs at ~3/4 the cost of an FFT multiply: selectors shared across outputs).
-bool decode_uses_matrix(uint64_t k, uint64_t m, uint32_t flags, uint64_t e, uint64_t present_count) {
+// Reconstruct kernel family for a pattern: 0 = FFT kernels (root.zig:268-335 as
+// written), 1 = matrix (e <= 8, one wave), 2 = output-tiled matrix (e <= 64).
+// The matrix kernels do k*e MACs at ~3/4 the cost of an FFT multiply (selectors
+// shared across outputs); the FFT register kernels exist for W <= 32 only, beyond
+// that the FFT path is the scratch-walking generic kernel (~10x slower per op).
+int decode_kind(uint64_t k, uint64_t m, uint32_t flags, uint64_t e, uint64_t present_count, uint64_t sb) {
   (void)flags;
   const std::string mode = decode_mode_env();
-  const bool can_matrix = e >= 1 && e <= kMatrixMaxOut && (k + m) <= 4096;
-  if (mode == "fft") return false;
-  if (mode == "matrix") return can_matrix;
-  return can_matrix && 3 * k * e <= 4 * fft_decode_mul_count(k, m, present_count, e);
+  if (mode == "fft" || e == 0 || (k + m) > 4096) return 0;
+  const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
+  const bool small_ok = e <= kMatrixMaxOut;
+  const bool tiled_ok = e <= kMtileMaxOut && sb % 512 == 0;
+  if (mode == "matrix") return small_ok ? 1 : tiled_ok ? 2 : 0;
+  uint64_t fft_cost = 4 * fft_decode_mul_count(k, m, present_count, e);
+  if (W > 32) fft_cost *= 10;  // generic kernel
+  if (3 * k * e > fft_cost) return 0;
+  return small_ok ? 1 : tiled_ok ? 2 : 0;
 }
 
 // root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
 // kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
-int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present,
+int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
                     std::shared_ptr<DecodePlan> &out) {
   const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                    std::to_string(flags) + "/" + mode + "/";
+                    std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::lock_guard<std::mutex> lk(g_plan_mu);
@@ -234,7 +243,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
   uint64_t e = 0, present_count = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
-  const bool use_matrix = decode_uses_matrix(k, m, flags, e, present_count);
+  const int kind = decode_kind(k, m, flags, e, present_count, sb);
+  const bool use_matrix = kind != 0;
 
   auto plan = std::make_shared<DecodePlan>();
   plan->work = static_cast<uint32_t>(W);
@@ -276,14 +286,18 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8
         scalar_reconstruct(sym.data(), received.data(), er.data(), k, m, d1);
         for (size_t j = 0; j < n_out; j++) img[(t * n_out + j) * 16 + b] = sym[out_pos[j]];
       }
-    std::vector<RsTab> tabs(n_in * n_out);
-    for (size_t i = 0; i < n_in * n_out; i++) tabs[i] = make_tab_from_images(&img[i * 16]);
+    // rows of n_out tables (kind 1) or padded to kMtileMaxOut zero tables (kind 2)
+    const size_t row = kind == 2 ? kMtileMaxOut : n_out;
+    std::vector<RsTab> tabs(n_in * row);
+    for (size_t t = 0; t < n_in; t++)
+      for (size_t j = 0; j < n_out; j++) tabs[t * row + j] = make_tab_from_images(&img[(t * n_out + j) * 16]);
     std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + n_in * sizeof(int32_t));
     std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
     std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), src.data(), n_in * sizeof(int32_t));
     int st = upload(blob.data(), blob.size(), dev, plan->buf);
     if (st) return st;
     plan->matrix = true;
+    plan->tiled = kind == 2;
     plan->e = static_cast<uint32_t>(n_out);
     plan->n_in = static_cast<uint32_t>(n_in);
     plan->off_mat = 0;
@@ -391,8 +405,11 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   uint64_t e = 0, have = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
-  if (decode_uses_matrix(k, m, flags_none(), e, have)) return choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name;
-  return choose_decode(k, m, sb, 4).name;
+  switch (decode_kind(k, m, flags_none(), e, have, sb)) {
+    case 1: return choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name;
+    case 2: return choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;
+    default: return choose_decode(k, m, sb, 4).name;
+  }
 }
 
 int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const void *d_original,
@@ -483,8 +500,10 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   int dev;
   if ((st = current_device(&dev))) return st;
   std::shared_ptr<DecodePlan> plan;
-  if ((st = get_decode_plan(dev, k, m, flags, present, plan))) return st;
-  const KernelChoice kc = plan->matrix ? choose_decode_matrix(plan->e, sb, max_nv) : choose_decode(k, m, sb, max_nv);
+  if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
+  const KernelChoice kc = plan->tiled    ? choose_decode_mtile(plan->e, sb, max_nv)
+                          : plan->matrix ? choose_decode_matrix(plan->e, sb, max_nv)
+                                         : choose_decode(k, m, sb, max_nv);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint8_t *base = static_cast<const uint8_t *>(plan->buf->p);
   DecodeArgs a{};

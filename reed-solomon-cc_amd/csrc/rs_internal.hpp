@@ -69,7 +69,7 @@ constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
 
 // Kernel variants: fused register-resident for small transforms, generic
 // (per-lane column walk over an HBM scratch work buffer) otherwise.
-enum class Variant { kRegister, kGeneric, kMatrix, kWaveSplit };
+enum class Variant { kRegister, kGeneric, kMatrix, kWaveSplit, kMatrixTiled };
 
 struct KernelChoice {
   Variant variant;
@@ -85,6 +85,10 @@ KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
 // reconstruct as an n_out x n_in matrix of GF(2)-linear maps (decode matrix + GF MAC)
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv);
 constexpr uint32_t kMatrixMaxOut = 8;
+// output-tiled matrix kernel: 4 waves x kMtileEW outputs
+constexpr int kMtileEW = 16;
+constexpr uint32_t kMtileMaxOut = 4 * kMtileEW;
+KernelChoice choose_decode_mtile(uint32_t n_out, uint64_t shard_bytes, int max_nv);
 
 hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
 hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s);

@@ -375,6 +375,52 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
   }
 }
 
+// ======================================= matrix reconstruct, output-tiled waves
+// For 8 < e <= 64 (e.g. RS(200,55) losing all 55 data shards it can): a
+// workgroup's 4 waves share the same 64 column units and split the e outputs,
+// EW per wave ("per-wave output-shard tiling"); each wave streams all k inputs
+// (the 4 waves read the same lines back to back: HBM once, L2 for the rest).
+template <int EW, int NV>
+__global__ __launch_bounds__(kBlock) void k_decode_mtile(DecodeArgs a) {
+  const uint64_t sb = a.shard_bytes;
+  if (blockIdx.x >= sb / 64 * (8 / NV) / 64) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t j0 = w * EW;
+  if (j0 >= a.n_out) return;  // no barriers in this kernel: idle waves may leave
+  const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
+  const uint64_t s = blockIdx.y;
+  typedef const __attribute__((address_space(4))) int32_t *CI;
+  const CI srcs = (CI)(a.pos_src);
+  const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
+  const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
+  auto in_ptr = [&](uint32_t i) {
+    const int32_t src = srcs[i];
+    return ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb;
+  };
+  const uint32_t stride = 4 * EW;  // padded outputs per table row
+  Sym<NV> acc[EW];
+#pragma unroll
+  for (int j = 0; j < EW; j++) dev::zero(acc[j]);
+  Sym<NV> y;
+  dev::load_sym(y, in_ptr(0), off, a.contig);
+  for (uint32_t i = 0; i < a.n_in; i++) {
+    Sym<NV> nxt = y;
+    if (i + 1 < a.n_in) dev::load_sym(nxt, in_ptr(i + 1), off, a.contig);
+    Sel<NV> sel;
+    make_sel(sel, y);
+    const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * stride + j0;
+    asm volatile("" : "+s"(row));
+#pragma unroll
+    for (int j = 0; j < EW; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
+    y = nxt;
+  }
+  uint8_t *out = a.out + s * a.out_stripe_stride;
+#pragma unroll
+  for (int j = 0; j < EW; j++)
+    if (j0 + j < a.n_out) dev::store_sym(out + static_cast<uint64_t>(j0 + j) * sb, off, acc[j], a.contig);
+}
+
 // ============================================ generic: column walk in HBM scratch
 template <int NV>
 __device__ __forceinline__ void ld(Sym<NV> &s, const uint8_t *p) {
@@ -688,12 +734,17 @@ KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_
   return kc;
 }
 
+KernelChoice choose_decode_mtile(uint32_t n_out, uint64_t shard_bytes, int max_nv) {
+  (void)n_out;
+  int nv = std::min(std::min(env_nv(1), max_nv), 2);
+  if (shard_bytes % (512ull * nv)) nv = 1;
+  return {Variant::kMatrixTiled, kMtileEW, nv, nv == 1 ? "decode_mtile16_nv1" : "decode_mtile16_nv2"};
+}
+
 #define RS_MAT_CASE(E_, NV_)                                                                  \
   if (kc.size == E_ && kc.nv == NV_) {                                                        \
     switch (kc.prefetch) {                                                                    \
       case 2: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 2>), grid, dim3(kBlock), 0, s, a); break; \
-      case 4: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 4>), grid, dim3(kBlock), 0, s, a); break; \
-      case 5: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 5>), grid, dim3(kBlock), 0, s, a); break; \
       default: hipLaunchKernelGGL((k_decode_matrix<E_, NV_, 1>), grid, dim3(kBlock), 0, s, a); break; \
     }                                                                                         \
     return hipGetLastError();                                                                 \
@@ -777,6 +828,13 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
     RS_DEC_CASE(16, 1) RS_DEC_CASE(16, 2) RS_DEC_CASE(16, 4)
     RS_DEC_CASE(32, 1) RS_DEC_CASE(32, 2)
     return hipErrorInvalidValue;
+  }
+  if (kc.variant == Variant::kMatrixTiled) {
+    const uint64_t regions = a.shard_bytes / 64 * (8 / kc.nv) / 64;
+    const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
+    if (kc.nv == 1) hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
+    return hipGetLastError();
   }
   if (kc.variant == Variant::kMatrix) {
     RS_MAT_NV(1) RS_MAT_NV(2) RS_MAT_NV(3) RS_MAT_NV(4)

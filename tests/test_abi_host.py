@@ -116,6 +116,7 @@ def test_device_entry_points_fail_loudly_without_gpu():
 def test_kernel_selection():
     assert R.encode_kernel_name(10, 4, 1 << 20) == "encode_reg_w4_nv4"
     assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "decode_matrix_e4_nv4"
-    assert R.reconstruct_kernel_name(200, 55, 1 << 18).startswith("decode_generic")
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "decode_mtile16_nv1"
+    assert R.reconstruct_kernel_name(200, 55, 320).startswith("decode_generic")
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"
     assert R.encode_kernel_name(100, 20, 1 << 18).startswith("encode_generic")
