@@ -126,6 +126,21 @@ int rs_reconstruct_batch_dev(uint64_t original_count, uint64_t recovery_count, s
                              uint64_t recovery_stripe_stride, void *d_restored, uint64_t restored_stripe_stride,
                              uint32_t flags, rs_stream_t stream);
 
+/* Reconstruct with a per-stripe erasure pattern (§8f rank 2). d_present: DEVICE
+ * array, n_stripes rows of k+m flags (row stride present_stride, 0 = k+m). The
+ * erasure locator (Generic.zig:200-215, two 64K-point FWHTs) is evaluated per
+ * stripe on the GPU. Stripe s restores its missing originals, ascending, into
+ * slots [0, e_s) of its d_restored row ([n][max_e][shard_bytes]); slots >= e_s
+ * are not written. d_status (device, n int32, may be NULL) receives per stripe
+ * RS_OK, RS_ERR_NOT_ENOUGH_SHARDS (< k present) or RS_ERR_INVALID_ARGUMENT
+ * (e_s > max_e: restored slots past max_e are dropped). */
+int rs_reconstruct_batch_dev_patterns(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                                      uint64_t n_stripes, const uint8_t *d_present, uint64_t present_stride,
+                                      uint32_t max_e, const void *d_original, uint64_t original_stripe_stride,
+                                      const void *d_recovery, uint64_t recovery_stripe_stride, void *d_restored,
+                                      uint64_t restored_stripe_stride, int32_t *d_status, uint32_t flags,
+                                      rs_stream_t stream);
+
 /* -------------------------------------- host-resident batches (end to end)
  * Same layouts and semantics as the *_dev calls, but the batch lives in HOST
  * memory: the library streams it through HBM in slices with a 3-deep

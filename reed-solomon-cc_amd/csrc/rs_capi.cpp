@@ -541,6 +541,10 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     b.orig += s0 * orig_stride;
     b.rec += s0 * rec_stride;
     b.out += s0 * out_stride;
+    b.tab_pre += s0 * a.pattern_stride;
+    b.tab_post += s0 * a.pattern_stride;
+    b.pos_src += s0 * a.pattern_stride;
+    b.pos_dst += s0 * a.pattern_stride;
     b.n_stripes = std::min(per, n_stripes - s0);
     b.scratch = static_cast<uint8_t *>(scratch);
     b.scratch_stripes = per;
@@ -551,6 +555,147 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     }
   }
   HIP_TRY(hipFreeAsync(scratch, s));
+  return RS_OK;
+}
+
+// ------------------------------------------------ per-stripe erasure patterns
+namespace {
+
+struct DeviceTables {  // exp, log, log_walsh in HBM (384 KiB per device)
+  std::shared_ptr<DevBuf> buf;
+};
+std::map<int, DeviceTables> g_dev_tables;
+
+int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_dev_tables.find(dev);
+  if (it == g_dev_tables.end()) {
+    const Tables &t = tables();
+    std::vector<uint16_t> blob(3 * kOrder);
+    std::memcpy(blob.data(), t.exp, kOrder * 2);
+    std::memcpy(blob.data() + kOrder, t.log, kOrder * 2);
+    std::memcpy(blob.data() + 2 * kOrder, t.log_walsh, kOrder * 2);
+    DeviceTables d;
+    int st = upload(blob.data(), blob.size() * 2, dev, d.buf);
+    if (st) return st;
+    it = g_dev_tables.emplace(dev, d).first;
+  }
+  const uint16_t *b = static_cast<const uint16_t *>(it->second.buf->p);
+  *exp = b;
+  *log = b + kOrder;
+  *lw = b + 2 * kOrder;
+  return RS_OK;
+}
+
+std::map<std::string, std::shared_ptr<DevBuf>> g_twiddle_plans;  // IFFT+FFT tables of size W, skew_delta 0
+
+int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft) {
+  const bool d1 = flags & RS_FLAG_QUIRK_D1;
+  std::vector<RsTab> tabs;
+  push_ifft_tabs(tabs, W, 0, d1);
+  off_fft = tabs.size() * sizeof(RsTab);
+  const std::string key = std::to_string(dev) + "/" + std::to_string(W) + "/" + std::to_string(d1);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_twiddle_plans.find(key);
+  if (it != g_twiddle_plans.end()) {
+    out = it->second;
+    return RS_OK;
+  }
+  push_fft_tabs(tabs, W, 0, d1);
+  int st = upload(tabs.data(), tabs.size() * sizeof(RsTab), dev, out);
+  if (st) return st;
+  g_twiddle_plans.emplace(key, out);
+  return RS_OK;
+}
+
+}  // namespace
+
+int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const uint8_t *d_present,
+                                      uint64_t present_stride, uint32_t max_e, const void *d_original,
+                                      uint64_t orig_stride, const void *d_recovery, uint64_t rec_stride,
+                                      void *d_restored, uint64_t out_stride, int32_t *d_status, uint32_t flags,
+                                      rs_stream_t stream) {
+  int st = check_codec(k, m, sb);
+  if (st) return st;
+  if (n_stripes == 0 || max_e == 0) return RS_OK;
+  if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");
+  if (present_stride == 0) present_stride = k + m;
+  if (orig_stride == 0) orig_stride = k * sb;
+  if (rec_stride == 0) rec_stride = m * sb;
+  if (out_stride == 0) out_stride = static_cast<uint64_t>(max_e) * sb;
+  const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
+                               reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
+  if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
+  int dev;
+  if ((st = current_device(&dev))) return st;
+  const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
+  const uint16_t *dexp, *dlog, *dlw;
+  if ((st = device_tables(dev, &dexp, &dlog, &dlw))) return st;
+  std::shared_ptr<DevBuf> tw;
+  size_t off_fft = 0;
+  if ((st = twiddle_plan(dev, W, flags, tw, off_fft))) return st;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // per-stripe plan: logs u16 | pre RsTab | post RsTab | src i32 | dst i32 (W entries each)
+  const uint64_t per = W * (2 + 2 * sizeof(RsTab) + 8);
+  void *tmp = nullptr;
+  HIP_TRY(hipMallocAsync(&tmp, n_stripes * per + 256, s));
+  uint8_t *base = static_cast<uint8_t *>(tmp);
+  RsTab *pre = reinterpret_cast<RsTab *>(base);
+  RsTab *post = pre + n_stripes * W;
+  int32_t *src = reinterpret_cast<int32_t *>(post + n_stripes * W);
+  int32_t *dst = src + n_stripes * W;
+  uint16_t *logs = reinterpret_cast<uint16_t *>(dst + n_stripes * W);
+  hipError_t e = launch_pattern_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
+                                     static_cast<uint32_t>(C), static_cast<uint32_t>(W), n_stripes, max_e,
+                                     flags & RS_FLAG_QUIRK_D1, dexp, dlog, dlw, logs, pre, post, src, dst, d_status,
+                                     s);
+  if (e != hipSuccess) {
+    (void)hipFreeAsync(tmp, s);
+    return hip_fail(e, "launch_pattern_plan");
+  }
+  const KernelChoice kc = choose_decode(k, m, sb, max_nv);
+  DecodeArgs a{};
+  a.orig = static_cast<const uint8_t *>(d_original);
+  a.orig_stripe_stride = orig_stride;
+  a.rec = static_cast<const uint8_t *>(d_recovery);
+  a.rec_stripe_stride = rec_stride;
+  a.out = static_cast<uint8_t *>(d_restored);
+  a.out_stripe_stride = out_stride;
+  a.shard_bytes = sb;
+  a.tab_ifft = static_cast<const RsTab *>(tw->p);
+  a.tab_fft = reinterpret_cast<const RsTab *>(static_cast<const uint8_t *>(tw->p) + off_fft);
+  a.tab_pre = pre;
+  a.tab_post = post;
+  a.pos_src = src;
+  a.pos_dst = dst;
+  a.work = static_cast<uint32_t>(W);
+  a.trunc = static_cast<uint32_t>(C + k);
+  a.pattern_stride = W;
+  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
+  if (kc.variant != Variant::kGeneric) {
+    a.n_stripes = n_stripes;
+    e = launch_decode(kc, a, s);
+  } else {
+    const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (W * sb)));
+    void *scratch = nullptr;
+    e = hipMallocAsync(&scratch, cap * W * sb, s);
+    for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += cap) {
+      DecodeArgs b = a;
+      b.orig += s0 * orig_stride;
+      b.rec += s0 * rec_stride;
+      b.out += s0 * out_stride;
+      b.tab_pre += s0 * W;
+      b.tab_post += s0 * W;
+      b.pos_src += s0 * W;
+      b.pos_dst += s0 * W;
+      b.n_stripes = std::min(cap, n_stripes - s0);
+      b.scratch = static_cast<uint8_t *>(scratch);
+      e = launch_decode(kc, b, s);
+    }
+    if (scratch) (void)hipFreeAsync(scratch, s);
+  }
+  (void)hipFreeAsync(tmp, s);
+  if (e != hipSuccess) return hip_fail(e, "launch_decode (patterns)");
   return RS_OK;
 }
 

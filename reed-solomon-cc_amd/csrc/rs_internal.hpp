@@ -63,6 +63,9 @@ struct DecodeArgs {
   uint32_t n_in;
   uint32_t n_out;
   bool contig;  // lane layout (dev::load_sym)
+  // per-stripe patterns: tab_pre/tab_post/pos_src/pos_dst advance by
+  // s * pattern_stride entries for stripe s (0 = one plan for the batch)
+  uint64_t pattern_stride;
 };
 constexpr int32_t kSrcRecovery = 0x40000000;
 constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
@@ -95,6 +98,12 @@ hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_
 
 // contiguous lane layout possible for this shard size and lane width?
 inline bool contig_ok(uint64_t shard_bytes, int nv) { return shard_bytes % (512ull * nv) == 0; }
+
+// Device-side plans for per-stripe erasure patterns (W entries per stripe)
+hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
+                               const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
+                               RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s);
 
 // Engine shims (generic, in place on a single-stripe work buffer)
 hipError_t launch_engine_fft(uint8_t *work, uint64_t shard_bytes, uint64_t pos, uint64_t size, uint64_t trunc,

@@ -114,15 +114,18 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
     const uint64_t s = blockIdx.y;
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
+    // shared plan, or this stripe's own (per-stripe erasure patterns)
+    const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride, *tab_post = a.tab_post + s * a.pattern_stride;
+    const int32_t *pos_src = a.pos_src + s * a.pattern_stride, *pos_dst = a.pos_dst + s * a.pattern_stride;
     Sym<NV> w[W];
     // erasure masks on received shards, zero elsewhere: root.zig:291-303
 #pragma unroll
     for (int p = 0; p < W; p++) {
-      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)a.pos_src)[p];
+      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)pos_src)[p];
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
         dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, off, a.contig);
-        dev::mul_inplace(w[p], dev::load_tab(a.tab_pre + p));
+        dev::mul_inplace(w[p], dev::load_tab(tab_pre + p));
       } else {
         dev::zero(w[p]);
       }
@@ -133,9 +136,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
     uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
     for (int p = 0; p < W; p++) {  // root.zig:321-326
-      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)a.pos_dst)[p];
+      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
       if (dst >= 0) {
-        dev::mul_inplace(w[p], dev::load_tab(a.tab_post + p));
+        dev::mul_inplace(w[p], dev::load_tab(tab_post + p));
         dev::store_sym(out + static_cast<uint64_t>(dst) * sb, off, w[p], a.contig);
       }
     }
@@ -587,13 +590,15 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
     uint8_t *work = a.scratch + s * W * sb + off;
+    const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride, *tab_post = a.tab_post + s * a.pattern_stride;
+    const int32_t *pos_src = a.pos_src + s * a.pattern_stride, *pos_dst = a.pos_dst + s * a.pattern_stride;
     for (uint64_t p = 0; p < W; p++) {
-      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)a.pos_src)[p];
+      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)pos_src)[p];
       Sym<NV> v;
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
         dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, a.contig);
-        dev::mul_inplace(v, dev::load_tab(a.tab_pre + p));
+        dev::mul_inplace(v, dev::load_tab(tab_pre + p));
       } else {
         dev::zero(v);
       }
@@ -607,15 +612,163 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
     fft_mem<NV>(work, sb, 0, W, a.trunc, a.tab_fft);
     uint8_t *out = a.out + s * a.out_stripe_stride + off;
     for (uint64_t p = 0; p < W; p++) {
-      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)a.pos_dst)[p];
+      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
       if (dst >= 0) {
         Sym<NV> v;
         ld(v, work + p * sb);
-        dev::mul_inplace(v, dev::load_tab(a.tab_post + p));
+        dev::mul_inplace(v, dev::load_tab(tab_post + p));
         dev::store_sym(out + static_cast<uint64_t>(dst) * sb, 0u, v, a.contig);
       }
     }
   }
+}
+
+// ================================== per-stripe erasure patterns: plans on device
+// (§8f rank 2) One workgroup per stripe evaluates the erasure locator exactly as
+// Generic.zig:200-215 does — FWHT truncated to chunk+k, pointwise product with
+// log_walsh mod 65535, full 65536-point FWHT (walsh_hadamard.zig:16-62) — on a
+// 128 KiB u16 array in LDS, then the stripe's W multiplier tables are built.
+__device__ __forceinline__ uint32_t add_mod_d(uint32_t x, uint32_t y) {
+  const uint32_t s = x + y;
+  return (s + (s >> 16)) & 0xFFFF;
+}
+__device__ __forceinline__ uint32_t sub_mod_d(uint32_t x, uint32_t y) {
+  const uint32_t d = x + 65535u - y;
+  return (d + (d >> 16)) & 0xFFFF;
+}
+
+// walsh_hadamard.zig:16-31 over LDS, groups r < m; all threads call
+__device__ void fwht_lds(uint16_t *e, uint32_t m) {
+  uint32_t dist = 1;
+  for (uint32_t stride = 4; stride <= 65536; dist = stride, stride *= 4) {
+    const uint32_t groups = (m + stride - 1) / stride;
+    const uint32_t total = groups * dist;
+    for (uint32_t t = threadIdx.x; t < total; t += blockDim.x) {
+      const uint32_t x0 = t / dist * stride + t % dist;
+      const uint32_t x1 = x0 + dist, x2 = x1 + dist, x3 = x2 + dist;
+      const uint32_t a0 = e[x0], a1 = e[x1], a2 = e[x2], a3 = e[x3];
+      const uint32_t s0 = add_mod_d(a0, a1), d0 = sub_mod_d(a0, a1);
+      const uint32_t s1 = add_mod_d(a2, a3), d1 = sub_mod_d(a2, a3);
+      e[x0] = static_cast<uint16_t>(add_mod_d(s0, s1));
+      e[x1] = static_cast<uint16_t>(add_mod_d(d0, d1));
+      e[x2] = static_cast<uint16_t>(sub_mod_d(s0, s1));
+      e[x3] = static_cast<uint16_t>(sub_mod_d(d0, d1));
+    }
+    __syncthreads();
+  }
+}
+
+// per stripe: present[k+m] -> logs[W] (root.zig:277-289 + Generic.zig:200-215)
+__global__ __launch_bounds__(1024) void k_erasure_logs(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                       uint32_t k, uint32_t m, uint32_t C, uint32_t W,
+                                                       const uint16_t *__restrict__ log_walsh,
+                                                       uint16_t *__restrict__ logs) {
+  __shared__ uint16_t e[65536];
+  const uint8_t *pr = present + static_cast<uint64_t>(blockIdx.x) * present_stride;
+  const uint32_t end = C + k;
+  for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x) {
+    uint16_t v = 0;
+    if (i < m) v = pr[k + i] ? 0 : 1;
+    else if (i < C) v = 1;
+    else if (i < end) v = pr[i - C] ? 0 : 1;
+    e[i] = v;
+  }
+  __syncthreads();
+  fwht_lds(e, end);
+  for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x) {
+    const uint32_t prod = static_cast<uint32_t>(e[i]) * log_walsh[i];
+    e[i] = static_cast<uint16_t>(add_mod_d(prod & 0xFFFF, prod >> 16));
+  }
+  __syncthreads();
+  fwht_lds(e, 65536);
+  for (uint32_t p = threadIdx.x; p < W; p += blockDim.x) logs[static_cast<uint64_t>(blockIdx.x) * W + p] = e[p];
+}
+
+__device__ __forceinline__ uint32_t mul16_d(uint32_t x, uint32_t lm, const uint16_t *exp, const uint16_t *log) {
+  return x == 0 ? 0 : exp[add_mod_d(log[x], lm)];
+}
+__device__ uint32_t mul_engine_d(uint32_t x, uint32_t lm, bool d1, const uint16_t *exp, const uint16_t *log) {
+  if (!d1) return mul16_d(x, lm, exp, log);
+  const uint32_t xh = ((x & 0xF) << 4) ^ (x & 0xFFF0);
+  return (mul16_d(x, lm, exp, log) & 0xFF) | (mul16_d(xh, lm, exp, log) & 0xFF00);
+}
+// rs_gf.cpp make_tab on device
+__device__ void make_tab_d(RsTab &t, uint32_t lm, bool d1, const uint16_t *exp, const uint16_t *log) {
+  constexpr int kOff[6] = {0, 3, 6, 8, 11, 14};
+  constexpr int kBits[6] = {3, 3, 2, 3, 3, 2};
+  constexpr int kSlot[6] = {0, 2, 4, 5, 7, 9};
+#pragma unroll
+  for (int i = 0; i < 10; i++) t.lo[i] = t.hi[i] = 0;
+#pragma unroll
+  for (int f = 0; f < 6; f++)
+    for (uint32_t v = 0; v < (1u << kBits[f]); v++) {
+      const uint32_t p = mul_engine_d(v << kOff[f], lm, d1, exp, log);
+      const int w = kSlot[f] + (v >> 2), sh = 8 * (v & 3);
+      t.lo[w] |= (p & 0xFF) << sh;
+      t.hi[w] |= (p >> 8) << sh;
+    }
+  t.flags = 0;
+  t.log_m = lm;
+  t.pad[0] = t.pad[1] = 0;
+}
+
+// per (stripe, position): masks, sources, restored slots (root.zig:291-326)
+__global__ __launch_bounds__(256) void k_pattern_tables(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                        uint32_t k, uint32_t m, uint32_t C, uint32_t W, uint32_t n,
+                                                        uint32_t max_e, bool d1, const uint16_t *__restrict__ logs,
+                                                        const uint16_t *__restrict__ exp, const uint16_t *__restrict__ log,
+                                                        RsTab *pre, RsTab *post, int32_t *src, int32_t *dst,
+                                                        int32_t *status) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= static_cast<uint64_t>(n) * W) return;
+  const uint64_t s = g / W;
+  const uint32_t p = static_cast<uint32_t>(g % W);
+  const uint8_t *pr = present + s * present_stride;
+  if (p == 0 && status) {  // root.zig:271 NotEnoughShards; restored slots beyond max_e: InvalidArgument
+    uint32_t have = 0, e = 0;
+    for (uint32_t i = 0; i < k + m; i++) have += pr[i] ? 1 : 0;
+    for (uint32_t i = 0; i < k; i++) e += pr[i] ? 0 : 1;
+    status[s] = have < k ? 2 : (e > max_e ? 14 : 0);
+  }
+  const uint32_t lm = logs[g];
+  int32_t sv = -1, dv = -1;
+  RsTab tp{}, tq{};
+  if (p < m && pr[k + p]) {
+    sv = kSrcRecovery | static_cast<int32_t>(p);
+    make_tab_d(tp, lm, d1, exp, log);
+  } else if (p >= C && p < C + k && pr[p - C]) {
+    sv = static_cast<int32_t>(p - C);
+    make_tab_d(tp, lm, d1, exp, log);
+  }
+  if (p >= C && p < C + k && !pr[p - C]) {
+    int32_t slot = 0;
+    for (uint32_t i = 0; i < p - C; i++) slot += pr[i] ? 0 : 1;
+    dv = slot < static_cast<int32_t>(max_e) ? slot : -1;
+    make_tab_d(tq, 65535u - lm, d1, exp, log);
+  }
+  pre[g] = tp;
+  post[g] = tq;
+  src[g] = sv;
+  dst[g] = dv;
+}
+
+hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
+                               const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
+                               RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
+  for (uint64_t s0 = 0; s0 < n; s0 += 65535) {
+    const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
+    hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, d_present + s0 * present_stride,
+                       present_stride, k, m, C, W, d_log_walsh, logs + s0 * W);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const uint64_t total = n * W;
+  const uint64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(k_pattern_tables, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, d_present,
+                     present_stride, k, m, C, W, static_cast<uint32_t>(n), max_e, d1, logs, d_exp, d_log, pre, post,
+                     src, dst, status);
+  return hipGetLastError();
 }
 
 // ========================================================== engine test shims
@@ -788,6 +941,10 @@ hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_
     b.orig += s0 * a.orig_stripe_stride;
     b.rec += s0 * a.rec_stripe_stride;
     b.out += s0 * a.out_stripe_stride;
+    b.tab_pre += s0 * a.pattern_stride;
+    b.tab_post += s0 * a.pattern_stride;
+    b.pos_src += s0 * a.pattern_stride;
+    b.pos_dst += s0 * a.pattern_stride;
     b.n_stripes = std::min<uint64_t>(65535, a.n_stripes - s0);
     hipError_t e = launch_decode_one(kc, b, s);
     if (e != hipSuccess) return e;

@@ -77,6 +77,8 @@ def lib():
         "rs_decoder_free": (None, [vp]),
         "rs_encode_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32, vp]),
         "rs_reconstruct_batch_dev": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32, vp]),
+        "rs_reconstruct_batch_dev_patterns": (C.c_int, [u64, u64, sz, u64, vp, u64, u32, vp, u64, vp, u64, vp, u64,
+                                                        vp, u32, vp]),
         "rs_encode_batch_host": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32]),
         "rs_reconstruct_batch_host": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32]),
         "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
@@ -274,6 +276,19 @@ def _host_ptr(a) -> int:
         return a.data_ptr()
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data
+
+
+def reconstruct_batch_dev_patterns(original_count: int, recovery_count: int, present, original, recovery,
+                                   restored, status=None, flags: int = FLAG_CORRECTED, stream=None):
+    """Per-stripe erasure patterns. present: uint8 CUDA tensor [n, k+m]; restored [n, max_e, sb];
+    status: optional int32 CUDA tensor [n] (0 ok, 2 NotEnoughShards, 14 too many erasures for max_e)."""
+    n, k, sb = original.shape
+    max_e = restored.shape[1]
+    _check(lib().rs_reconstruct_batch_dev_patterns(
+        original_count, recovery_count, sb, n, C.c_void_p(present.data_ptr()), present.stride(0), max_e,
+        C.c_void_p(original.data_ptr()), original.stride(0), C.c_void_p(recovery.data_ptr()), recovery.stride(0),
+        C.c_void_p(restored.data_ptr()), restored.stride(0),
+        C.c_void_p(status.data_ptr()) if status is not None else None, flags, _stream_handle(stream)))
 
 
 def encode_kernel_name(k, m, shard_bytes) -> str:

@@ -297,3 +297,38 @@ def test_host_batch_pipeline(oracle, pinned):
     out = torch.zeros((n, len(missing), sb), dtype=torch.uint8)
     R.reconstruct_batch_host(k, m, present, data, par, out)
     assert (out.numpy() == data.numpy()[:, missing]).all()
+
+
+@pytest.mark.parametrize("k,m,sb", [(10, 4, 4096), (5, 5, 320), (4, 2, 2048), (16, 16, 1024), (20, 16, 512),
+                                    (200, 55, 512)])
+@pytest.mark.parametrize("flags", [0, 1])
+def test_reconstruct_per_stripe_patterns(oracle, k, m, sb, flags):
+    """rs_reconstruct_batch_dev_patterns: erasure locator per stripe on the GPU (LDS FWHT)."""
+    n = 9
+    rng = np.random.default_rng(k * 31 + m + flags)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags)
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n):
+        lost = rng.choice(k + m, size=int(rng.integers(0, m + 1)), replace=False)
+        present[s, lost] = 0
+    present[n - 1, :] = 1
+    present[n - 1, :m + 1] = 0  # not enough shards
+    max_e = m
+    out = torch.zeros((n, max_e, sb), dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
+    torch.cuda.synchronize()
+    out = out.cpu().numpy()
+    status = status.cpu().numpy()
+    assert status[n - 1] == 2
+    for s in range(n - 1):
+        assert status[s] == 0, s
+        missing = [i for i in range(k) if not present[s, i]]
+        if not missing:
+            continue
+        exp = oracle.reconstruct_batch(k, m, present[s], np.concatenate([data[s:s + 1], par[s:s + 1]], axis=1),
+                                       quirks=flags)
+        assert (out[s, :len(missing)] == exp[0]).all(), (s, missing)
+        if flags == 0:
+            assert (out[s, :len(missing)] == data[s, missing]).all()
