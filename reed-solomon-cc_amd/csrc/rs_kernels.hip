@@ -752,10 +752,10 @@ __global__ __launch_bounds__(256) void k_pattern_tables(const uint8_t *__restric
   dst[g] = dv;
 }
 
-hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
-                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
-                               const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
-                               RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
+hipError_t launch_pattern_plan_impl(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m,
+                                    uint32_t C, uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
+                                    const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
+                                    RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
   for (uint64_t s0 = 0; s0 < n; s0 += 65535) {
     const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
     hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, d_present + s0 * present_stride,
@@ -1000,6 +1000,14 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
   }
   hipLaunchKernelGGL(k_decode_generic<1>, grid, dim3(kBlock), 0, s, a);
   return hipGetLastError();
+}
+
+hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
+                               const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
+                               RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
+  return launch_pattern_plan_impl(d_present, present_stride, k, m, C, W, n, max_e, d1, d_exp, d_log, d_log_walsh,
+                                  logs, pre, post, src, dst, status, s);
 }
 
 hipError_t launch_engine_fft(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
