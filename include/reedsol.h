@@ -44,7 +44,7 @@ typedef enum rs_status {
   RS_ERR_OUT_OF_MEMORY = 10,           /* allocator failure */
   RS_ERR_OVERFLOW = 11,                /* std.math.ceilPowerOfTwo */
   RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO") */
-  RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* shard_bytes % 64 != 0: root.zig:385 @panic("TODO") */
+  RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* root.zig:385 @panic("TODO"); here only rs_reconstruct_batch_dev_patterns */
   RS_ERR_INVALID_ARGUMENT = 14,        /* NULL pointer / bad stride */
   RS_ERR_DEVICE = 15,                  /* HIP runtime error (message: rs_last_error()) */
   RS_ERR_NO_DEVICE = 16,               /* no gfx950 device visible */
@@ -67,8 +67,10 @@ int rs_use_high_rate(uint64_t original_count, uint64_t recovery_count);
 
 /* ------------------------------------------- one-shot host API (root.zig:14-84)
  * Host buffers in, host buffers out; internally H2D -> fused HIP kernel -> D2H.
- * Generalises the reference's 64-byte-typed result to any shard_bytes % 64 == 0
- * (defect D6). Caller owns every buffer. */
+ * Generalises the reference's 64-byte-typed result to any even shard_bytes
+ * (defect D6); a tail of shard_bytes % 64 bytes is coded as one more chunk in the
+ * layout undoLastChunkEncoding implies (root.zig:338-348; the reference itself
+ * panics on tails, root.zig:385). Caller owns every buffer. */
 
 /* replaces `encode(allocator, original_count, recovery_count, original)` root.zig:14-30.
  * original[k] -> recovery_out[m] (each shard_bytes). */

@@ -464,8 +464,35 @@ static int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
   if (hr < 0) return -hr;
   if (hr == 0) return RSO_ERR_LOW_RATE_UNSUPPORTED; /* root.zig:120 @panic("TODO") */
   if (shard_bytes == 0 || (shard_bytes & 1)) return RSO_ERR_INVALID_SHARD_SIZE; /* root.zig:103 */
-  if (shard_bytes % 64) return RSO_ERR_SHARD_TAIL_UNSUPPORTED;                  /* root.zig:384-386 */
+  /* shard_bytes % 64 != 0: the reference panics (root.zig:384-386); the oracle
+   * implements the tail layout its undoLastChunkEncoding (root.zig:338-348) implies. */
   return RSO_OK;
+}
+
+/* Shards.insert (root.zig:373-387) for one shard of sb bytes into L = ceil(sb/64)
+ * chunks. A tail of t bytes (t even, < 64) goes into the last chunk as
+ * [0, t/2) -> lo bytes [0, t/2) and [t/2, t) -> hi bytes [32, 32 + t/2), the rest
+ * zero — the inverse of undoLastChunkEncoding's memmove (root.zig:346). */
+static void insert_shard(uint8_t *dst, const uint8_t *src, size_t sb) {
+  const size_t whole = sb / 64 * 64, t = sb % 64;
+  memcpy(dst, src, whole);
+  if (t) {
+    uint8_t *c = dst + whole;
+    memset(c, 0, 64);
+    memcpy(c, src + whole, t / 2);
+    memcpy(c + 32, src + whole + t / 2, t / 2);
+  }
+}
+
+/* copy out + undoLastChunkEncoding (root.zig:338-348, with the memmove applied to
+ * the buffer itself rather than to a copy, defect D7) */
+static void extract_shard(uint8_t *dst, const uint8_t *src, size_t sb) {
+  const size_t whole = sb / 64 * 64, t = sb % 64;
+  memcpy(dst, src, whole);
+  if (t) {
+    memcpy(dst + whole, src + whole, t / 2);
+    memcpy(dst + whole + t / 2, src + whole + 32, t / 2);
+  }
 }
 
 /* Encoder.encode on a prepared work buffer (root.zig:136-173).
@@ -493,21 +520,21 @@ static void encode_work(uint8_t *work, size_t L, uint64_t k, uint64_t m, int qui
   rso_fft(work, L, 0, chunk, m, 0, quirks); /* root.zig:169 */
 }
 
-/* top-level encode (root.zig:14-30) generalised to shard_bytes % 64 == 0 */
+/* top-level encode (root.zig:14-30) generalised to any even shard_bytes */
 int rso_encode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,
                uint8_t *const *recovery_out, int quirks) {
   rso_init();
   if (k == 0 || original == NULL) return RSO_ERR_TOO_FEW_ORIGINAL_SHARDS;
   int st = check_codec(k, m, shard_bytes);
   if (st) return st;
-  size_t L = shard_bytes / 64;
+  size_t L = (shard_bytes + 63) / 64; /* root.zig:115 divCeil */
   uint64_t chunk = ceil_pow2(m);
   uint64_t work_count = (k + chunk - 1) / chunk * chunk; /* root.zig:106 */
   uint8_t *work = calloc(work_count * L, 64);
   if (!work) return RSO_ERR_OUT_OF_MEMORY;
-  for (uint64_t i = 0; i < k; i++) memcpy(SHARD(work, L, i), original[i], shard_bytes); /* Shards.insert */
+  for (uint64_t i = 0; i < k; i++) insert_shard(SHARD(work, L, i), original[i], shard_bytes); /* Shards.insert */
   encode_work(work, L, k, m, quirks);
-  for (uint64_t r = 0; r < m; r++) memcpy(recovery_out[r], SHARD(work, L, r), shard_bytes);
+  for (uint64_t r = 0; r < m; r++) extract_shard(recovery_out[r], SHARD(work, L, r), shard_bytes);
   free(work);
   return RSO_OK;
 }
@@ -547,7 +574,7 @@ static void decode_work(uint8_t *work, size_t L, uint64_t k, uint64_t m, const u
     if (!received[i]) rso_mul_scalar(SHARD(work, L, i), L, (uint16_t)(GF_MODULUS - erasures[i]), quirks);
 }
 
-/* top-level decode (root.zig:32-84) generalised to shard_bytes % 64 == 0 */
+/* top-level decode (root.zig:32-84) generalised to any even shard_bytes */
 int rso_decode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,
                const uint8_t *const *recovery, uint8_t *const *restored_out, int quirks) {
   rso_init();
@@ -562,7 +589,7 @@ int rso_decode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const 
   int st = check_codec(k, m, shard_bytes);
   if (st) return st;
   if (orig_present + rec_present < k) return RSO_ERR_NOT_ENOUGH_SHARDS; /* root.zig:271 */
-  size_t L = shard_bytes / 64;
+  size_t L = (shard_bytes + 63) / 64;
   uint64_t chunk = ceil_pow2(m);
   uint64_t work_count = ceil_pow2(chunk + k); /* root.zig:204 */
   uint8_t *work = calloc(work_count * L, 64);
@@ -576,17 +603,18 @@ int rso_decode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const 
   }
   for (uint64_t i = 0; i < k; i++)
     if (original[i]) {
-      memcpy(SHARD(work, L, chunk + i), original[i], shard_bytes);
+      insert_shard(SHARD(work, L, chunk + i), original[i], shard_bytes);
       received[chunk + i] = 1;
     }
   for (uint64_t i = 0; i < m; i++)
     if (recovery[i]) {
-      memcpy(SHARD(work, L, i), recovery[i], shard_bytes);
+      insert_shard(SHARD(work, L, i), recovery[i], shard_bytes);
       received[i] = 1;
     }
   decode_work(work, L, k, m, received, erasures, quirks);
   for (uint64_t i = 0; i < k; i++) /* root.zig:76-81 */
-    memcpy(restored_out[i], original[i] ? original[i] : SHARD(work, L, chunk + i), shard_bytes);
+    if (original[i]) memcpy(restored_out[i], original[i], shard_bytes);
+    else extract_shard(restored_out[i], SHARD(work, L, chunk + i), shard_bytes);
   free(work);
   free(received);
   free(erasures);
@@ -607,7 +635,7 @@ typedef struct {
 
 static void *batch_worker(void *arg) {
   batch_job *j = arg;
-  size_t L = j->shard_bytes / 64, sb = j->shard_bytes;
+  size_t L = (j->shard_bytes + 63) / 64, sb = j->shard_bytes;
   uint64_t k = j->k, m = j->m, chunk = ceil_pow2(m);
   if (j->op == 0) {
     uint64_t wc = (k + chunk - 1) / chunk * chunk;
@@ -618,9 +646,9 @@ static void *batch_worker(void *arg) {
     }
     for (size_t s = j->s_begin; s < j->s_end; s++) {
       const uint8_t *src = j->in + s * k * sb;
-      memcpy(work, src, k * sb); /* addOriginalShard x k */
+      for (uint64_t i = 0; i < k; i++) insert_shard(SHARD(work, L, i), src + i * sb, sb); /* addOriginalShard x k */
       encode_work(work, L, k, m, j->quirks);
-      memcpy(j->out + s * m * sb, work, m * sb);
+      for (uint64_t r = 0; r < m; r++) extract_shard(j->out + (s * m + r) * sb, SHARD(work, L, r), sb);
     }
     free(work);
   } else {
@@ -635,18 +663,18 @@ static void *batch_worker(void *arg) {
       memset(received, 0, wc);
       for (uint64_t i = 0; i < k; i++)
         if (j->present[i]) {
-          memcpy(SHARD(work, L, chunk + i), src + i * sb, sb);
+          insert_shard(SHARD(work, L, chunk + i), src + i * sb, sb);
           received[chunk + i] = 1;
         }
       for (uint64_t i = 0; i < m; i++)
         if (j->present[k + i]) {
-          memcpy(SHARD(work, L, i), src + (k + i) * sb, sb);
+          insert_shard(SHARD(work, L, i), src + (k + i) * sb, sb);
           received[i] = 1;
         }
       decode_work(work, L, k, m, received, erasures, j->quirks);
       uint64_t o = 0;
       for (uint64_t i = 0; i < k; i++)
-        if (!j->present[i]) memcpy(j->out + (s * e + o++) * sb, SHARD(work, L, chunk + i), sb);
+        if (!j->present[i]) extract_shard(j->out + (s * e + o++) * sb, SHARD(work, L, chunk + i), sb);
     }
     free(work);
     free(received);

@@ -51,7 +51,7 @@ enum {
   RSO_ERR_TOO_MANY_SHARDS = 9,
   RSO_ERR_OUT_OF_MEMORY = 10,
   RSO_ERR_LOW_RATE_UNSUPPORTED = 12,
-  RSO_ERR_SHARD_TAIL_UNSUPPORTED = 13,
+  RSO_ERR_SHARD_TAIL_UNSUPPORTED = 13, /* no longer returned: tails use the layout of root.zig:338-348 */
 };
 
 void rso_init(void);
@@ -82,7 +82,8 @@ void rso_eval_poly(uint16_t *erasures, uint64_t trunc);
 /* rate selection (root.zig:397-415): 1 = high rate, 0 = low rate, <0 = -error */
 int rso_use_high_rate(uint64_t k, uint64_t m);
 
-/* codec (root.zig) — caller owns every buffer; shard_bytes % 64 == 0 */
+/* codec (root.zig) — caller owns every buffer; any even shard_bytes (a tail of
+ * shard_bytes % 64 bytes uses the last-chunk layout root.zig:338-348 implies) */
 int rso_encode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,
                uint8_t *const *recovery_out, int quirks);
 /* original[i] / recovery[i] == NULL marks a missing shard; restored_out has k

@@ -81,7 +81,8 @@ int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
   if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
   if (hr == 0) return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec (reference panics, root.zig:120)");
   if (shard_bytes == 0 || (shard_bytes & 1)) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes is 0 or odd");
-  if (shard_bytes % 64) return fail(RS_ERR_SHARD_TAIL_UNSUPPORTED, "shard_bytes % 64 != 0 (reference panics, root.zig:385)");
+  // shard_bytes % 64 != 0: the reference panics (root.zig:385); handled here with
+  // the tail layout of root.zig:338-348 (tail_* below).
   return RS_OK;
 }
 
@@ -356,6 +357,82 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
 
 constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
 
+// ---------------------------------------------------------- shard tails
+// Batches whose shard_bytes is not a multiple of 64 run on padded copies
+// ([stripe][shard][ceil(sb/64)*64], tail chunk in the reference's layout) in
+// slices of <= 1 GiB, then the outputs are unpadded.
+constexpr uint64_t kTailSliceBytes = 1ull << 30;
+
+int pad_shards(const uint8_t *src, uint64_t src_stripe_stride, uint64_t sb, uint8_t *dst, uint64_t dst_stripe_stride,
+               uint64_t psb, uint64_t n, hipStream_t s) {
+  const uint64_t whole = sb / 64 * 64;
+  if (whole) HIP_TRY(hipMemcpy2DAsync(dst, dst_stripe_stride, src, src_stripe_stride, whole, n, hipMemcpyDeviceToDevice, s));
+  (void)psb;
+  HIP_TRY(launch_tail_pack(src, src_stripe_stride, dst, dst_stripe_stride, sb, n, false, s));
+  return RS_OK;
+}
+
+int unpad_shards(const uint8_t *src, uint64_t src_stripe_stride, uint64_t sb, uint8_t *dst, uint64_t dst_stripe_stride,
+                 uint64_t n, hipStream_t s) {
+  const uint64_t whole = sb / 64 * 64;
+  if (whole) HIP_TRY(hipMemcpy2DAsync(dst, dst_stripe_stride, src, src_stripe_stride, whole, n, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(launch_tail_pack(src, src_stripe_stride, dst, dst_stripe_stride, sb, n, true, s));
+  return RS_OK;
+}
+
+}  // namespace
+
+extern "C" int rs_encode_batch_dev(uint64_t, uint64_t, size_t, uint64_t, const void *, uint64_t, void *, uint64_t,
+                                   uint32_t, rs_stream_t);
+extern "C" int rs_reconstruct_batch_dev(uint64_t, uint64_t, size_t, uint64_t, const uint8_t *, const void *, uint64_t,
+                                        const void *, uint64_t, void *, uint64_t, uint32_t, rs_stream_t);
+
+namespace {
+
+int encode_tail(uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *orig, uint64_t ostride, uint8_t *rec,
+                uint64_t rstride, uint32_t flags, hipStream_t s) {
+  const uint64_t psb = (sb + 63) / 64 * 64;
+  const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n, kTailSliceBytes / ((k + m) * psb)));
+  void *buf = nullptr;
+  HIP_TRY(hipMallocAsync(&buf, cap * (k + m) * psb, s));
+  uint8_t *pin = static_cast<uint8_t *>(buf), *pout = pin + cap * k * psb;
+  int st = RS_OK;
+  for (uint64_t s0 = 0; st == RS_OK && s0 < n; s0 += cap) {
+    const uint64_t cnt = std::min(cap, n - s0);
+    for (uint64_t i = 0; st == RS_OK && i < k; i++)
+      st = pad_shards(orig + s0 * ostride + i * sb, ostride, sb, pin + i * psb, k * psb, psb, cnt, s);
+    if (st == RS_OK) st = rs_encode_batch_dev(k, m, psb, cnt, pin, 0, pout, 0, flags, s);
+    for (uint64_t r = 0; st == RS_OK && r < m; r++)
+      st = unpad_shards(pout + r * psb, m * psb, sb, rec + s0 * rstride + r * sb, rstride, cnt, s);
+  }
+  (void)hipFreeAsync(buf, s);
+  return st;
+}
+
+int reconstruct_tail(uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *present, uint64_t e,
+                     const uint8_t *orig, uint64_t ostride, const uint8_t *rec, uint64_t rstride, uint8_t *out,
+                     uint64_t outstride, uint32_t flags, hipStream_t s) {
+  const uint64_t psb = (sb + 63) / 64 * 64;
+  const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n, kTailSliceBytes / ((k + m + e) * psb)));
+  void *buf = nullptr;
+  HIP_TRY(hipMallocAsync(&buf, cap * (k + m + e) * psb, s));
+  uint8_t *po = static_cast<uint8_t *>(buf), *pr = po + cap * k * psb, *pout = pr + cap * m * psb;
+  int st = RS_OK;
+  for (uint64_t s0 = 0; st == RS_OK && s0 < n; s0 += cap) {
+    const uint64_t cnt = std::min(cap, n - s0);
+    for (uint64_t i = 0; st == RS_OK && i < k; i++)  // only present shards are read
+      if (present[i]) st = pad_shards(orig + s0 * ostride + i * sb, ostride, sb, po + i * psb, k * psb, psb, cnt, s);
+    for (uint64_t i = 0; st == RS_OK && i < m; i++)
+      if (present[k + i])
+        st = pad_shards(rec + s0 * rstride + i * sb, rstride, sb, pr + i * psb, m * psb, psb, cnt, s);
+    if (st == RS_OK) st = rs_reconstruct_batch_dev(k, m, psb, cnt, present, po, 0, pr, 0, pout, 0, flags, s);
+    for (uint64_t j = 0; st == RS_OK && j < e; j++)
+      st = unpad_shards(pout + j * psb, e * psb, sb, out + s0 * outstride + j * sb, outstride, cnt, s);
+  }
+  (void)hipFreeAsync(buf, s);
+  return st;
+}
+
 }  // namespace
 
 // ===================================================================== ABI
@@ -422,6 +499,12 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
   if (!d_original || !d_recovery) return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
   if (orig_stride == 0) orig_stride = k * sb;
   if (rec_stride == 0) rec_stride = m * sb;
+  if (sb % 64) {
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    return encode_tail(k, m, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride,
+                       static_cast<uint8_t *>(d_recovery), rec_stride, flags, static_cast<hipStream_t>(stream));
+  }
   if (orig_stride < k * sb || rec_stride < m * sb) return fail(RS_ERR_INVALID_ARGUMENT, "stripe stride too small");
   const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
                                orig_stride, rec_stride});
@@ -493,6 +576,13 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   if (out_stride == 0) out_stride = e * sb;
   if ((have && !d_original) || (have_rec && !d_recovery) || !d_restored)
     return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
+  if (sb % 64) {
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    return reconstruct_tail(k, m, sb, n_stripes, present, e, static_cast<const uint8_t *>(d_original), orig_stride,
+                            static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
+                            out_stride, flags, static_cast<hipStream_t>(stream));
+  }
   const int max_nv =
       align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
                 reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
@@ -619,6 +709,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
   if (st) return st;
   if (n_stripes == 0 || max_e == 0) return RS_OK;
   if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");
+  if (sb % 64) return fail(RS_ERR_SHARD_TAIL_UNSUPPORTED, "per-stripe patterns need shard_bytes % 64 == 0");
   if (present_stride == 0) present_stride = k + m;
   if (orig_stride == 0) orig_stride = k * sb;
   if (rec_stride == 0) rec_stride = m * sb;

@@ -105,6 +105,10 @@ hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride
                                const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
                                RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s);
 
+// Shard tails: pack one shard's last partial chunk into / out of the padded layout
+hipError_t launch_tail_pack(const uint8_t *src, uint64_t src_stripe_stride, uint8_t *dst, uint64_t dst_stripe_stride,
+                            uint64_t sb, uint64_t n, bool unpack, hipStream_t s);
+
 // Engine shims (generic, in place on a single-stripe work buffer)
 hipError_t launch_engine_fft(uint8_t *work, uint64_t shard_bytes, uint64_t pos, uint64_t size, uint64_t trunc,
                              const RsTab *tabs, bool inverse, hipStream_t s);

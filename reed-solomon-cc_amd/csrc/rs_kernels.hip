@@ -771,6 +771,33 @@ hipError_t launch_pattern_plan_impl(const uint8_t *d_present, uint64_t present_s
   return hipGetLastError();
 }
 
+// ======================================================= shard tails (sb % 64)
+// The reference panics on tails (root.zig:385); its undoLastChunkEncoding
+// (root.zig:338-348) implies the layout: a tail of t bytes is coded as one more
+// chunk with bytes [0,t/2) as lo bytes [0,t/2) and [t/2,t) as hi bytes
+// [32,32+t/2). Pack/unpack one shard's tail chunk for n stripes (one thread per
+// byte of the 64-B chunk); whole chunks are moved with hipMemcpy2DAsync.
+__global__ __launch_bounds__(256) void k_tail_pack(const uint8_t *__restrict__ src, uint64_t src_stripe_stride,
+                                                   uint8_t *__restrict__ dst, uint64_t dst_stripe_stride,
+                                                   uint64_t sb, uint64_t n, int unpack) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= n * 64) return;
+  const uint64_t s = g / 64;
+  const uint32_t j = static_cast<uint32_t>(g % 64);
+  const uint32_t t = static_cast<uint32_t>(sb % 64), h = t / 2;
+  const uint64_t whole = sb - t;
+  if (!unpack) {  // real shard (sb bytes) -> padded tail chunk
+    const uint8_t *in = src + s * src_stripe_stride + whole;
+    uint8_t v = 0;
+    if (j < h) v = in[j];
+    else if (j >= 32 && j < 32 + h) v = in[h + j - 32];
+    dst[s * dst_stripe_stride + whole + j] = v;
+  } else if (j < t) {  // padded tail chunk -> real shard
+    const uint8_t *in = src + s * src_stripe_stride + whole;
+    dst[s * dst_stripe_stride + whole + j] = j < h ? in[j] : in[32 + j - h];
+  }
+}
+
 // ========================================================== engine test shims
 __global__ __launch_bounds__(kBlock) void k_engine_transform(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size,
                                                              uint64_t trunc, const RsTab *tabs, int inverse) {
@@ -1008,6 +1035,15 @@ hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride
                                RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
   return launch_pattern_plan_impl(d_present, present_stride, k, m, C, W, n, max_e, d1, d_exp, d_log, d_log_walsh,
                                   logs, pre, post, src, dst, status, s);
+}
+
+hipError_t launch_tail_pack(const uint8_t *src, uint64_t src_stripe_stride, uint8_t *dst, uint64_t dst_stripe_stride,
+                            uint64_t sb, uint64_t n, bool unpack, hipStream_t s) {
+  if (sb % 64 == 0 || n == 0) return hipSuccess;
+  const uint64_t blocks = (n * 64 + 255) / 256;
+  hipLaunchKernelGGL(k_tail_pack, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, src, src_stripe_stride, dst,
+                     dst_stripe_stride, sb, n, unpack ? 1 : 0);
+  return hipGetLastError();
 }
 
 hipError_t launch_engine_fft(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size, uint64_t trunc,

@@ -332,3 +332,20 @@ def test_reconstruct_per_stripe_patterns(oracle, k, m, sb, flags):
         assert (out[s, :len(missing)] == exp[0]).all(), (s, missing)
         if flags == 0:
             assert (out[s, :len(missing)] == data[s, missing]).all()
+
+
+@pytest.mark.parametrize("sb", [2, 6, 66, 70, 1000, 4102])
+@pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (200, 55)])
+def test_shard_tails_vs_oracle(oracle, k, m, sb):
+    """shard_bytes % 64 != 0 (the reference panics): tail chunk layout of root.zig:338-348."""
+    rng = np.random.default_rng(sb * 7 + k)
+    n = 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = gpu_encode(k, m, data)
+    exp = oracle.encode_batch(k, m, data)
+    assert (par == exp).all()
+    present = np.ones(k + m, np.uint8)
+    lost = rng.choice(k, size=min(m, k), replace=False)
+    present[lost] = 0
+    got = gpu_reconstruct(k, m, present, data, par)
+    assert (got == data[:, sorted(lost)]).all()
