@@ -159,12 +159,22 @@ int rs_reconstruct_batch_host(uint64_t original_count, uint64_t recovery_count, 
                               uint64_t recovery_stripe_stride, void *h_restored, uint64_t restored_stripe_stride,
                               uint32_t flags);
 
-/* Which device kernel a call would run on ("encode_reg_w4_nv4", "decode_matrix_e4_nv4",
- * "encode_generic_nv1", ...), assuming 16-byte aligned buffers. present: k+m flags as
- * for rs_reconstruct_batch_dev, or NULL for "the first min(k, m) originals lost". */
+/* Which device kernel a call would run on ("net_i10_o4", "encode_reg_w4_nv4",
+ * "decode_matrix_e4_nv4", "encode_generic_nv1", ...), assuming 16-byte aligned buffers.
+ * present: k+m flags as for rs_reconstruct_batch_dev, or NULL for "the first min(k, m)
+ * originals lost". net_* = bit-sliced XOR network generated for the plan and compiled
+ * with hipRTC on first use (shard_bytes a multiple of 4096, <= 16 outputs; disable
+ * with RS_AMD_JIT=0). */
 const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
 const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                        const uint8_t *present);
+
+/* Plan-time network kernel: generate the bit-sliced network of an encode (present
+ * == NULL) or of one reconstruct pattern and compile it with hipRTC for gfx950, without
+ * loading it (no device needed: a build check). *compile_ms (optional) = compile time.
+ * RS_ERR_INVALID_ARGUMENT if the shape has no network form, RS_ERR_DEVICE if hipRTC fails. */
+int rs_net_compile_check(uint64_t original_count, uint64_t recovery_count, const uint8_t *present,
+                         uint32_t flags, double *compile_ms);
 
 /* ---------------------------------------- Engine seam (Generic.zig), test shim
  * The reference's comptime Engine interface (root.zig:10-12) at per-call

@@ -19,6 +19,7 @@
 #include "../../include/reedsol.h"
 #include "rs_gf.hpp"
 #include "rs_internal.hpp"
+#include "rs_jit.hpp"
 
 using namespace rs;
 
@@ -110,9 +111,17 @@ struct DevBuf {
   }
 };
 
+// Bit-sliced network kernel of a plan (rs_jit.hpp), compiled on first use.
+struct NetSlot {
+  std::mutex mu;
+  bool failed = false;
+  jit::NetSpec spec;
+};
+
 struct EncodePlan {
   std::shared_ptr<DevBuf> buf;
   uint32_t chunk, n_chunks, trunc_first, trunc_last, tabs_per_chunk, work;
+  std::shared_ptr<NetSlot> net = std::make_shared<NetSlot>();
 };
 
 struct DecodePlan {
@@ -121,7 +130,23 @@ struct DecodePlan {
   bool tiled = false;
   uint32_t work = 0, chunk = 0, trunc = 0, e = 0, n_in = 0;
   size_t off_fft = 0, off_pre = 0, off_post = 0, off_src = 0, off_dst = 0, off_mat = 0;  // byte offsets into buf
+  std::shared_ptr<NetSlot> net;  // set when the pattern runs as a bit-sliced network
 };
+
+// Compile (once) and return the plan's network kernel; nullptr if hipRTC failed
+// (the caller then runs the precompiled table-driven kernels).
+// (jit::get caches by content and code-shape knobs; a failure is reported once per plan.)
+const jit::Kernel *net_kernel(NetSlot &slot) {
+  std::lock_guard<std::mutex> lk(slot.mu);
+  if (slot.failed) return nullptr;
+  std::string err;
+  const jit::Kernel *k = jit::get(slot.spec, err);
+  if (!k) {
+    slot.failed = true;
+    std::fprintf(stderr, "[rs_amd] bit-sliced network unavailable, using table kernels: %s\n", err.c_str());
+  }
+  return k;
+}
 
 std::mutex g_plan_mu;
 std::map<std::string, std::shared_ptr<EncodePlan>> g_enc_plans;
@@ -136,6 +161,70 @@ int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out
   return RS_OK;
 }
 
+// The encode as a k -> m map of GF(2)-linear 16x16 maps: images of every basis
+// symbol of every data shard through Encoder.encode (root.zig:136-173).
+void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
+  const bool d1 = flags & RS_FLAG_QUIRK_D1, d2 = flags & RS_FLAG_QUIRK_D2;
+  ns.n_in = static_cast<uint32_t>(k);
+  ns.n_out = static_cast<uint32_t>(m);
+  ns.src.clear();
+  ns.images.assign(k * m * 16, 0);
+  std::vector<uint16_t> in(k, 0), out(m);
+  for (uint64_t t = 0; t < k; t++) {
+    ns.src.push_back(static_cast<int32_t>(t));
+    for (int b = 0; b < 16; b++) {
+      in[t] = static_cast<uint16_t>(1u << b);
+      scalar_encode(in.data(), k, m, d1, d2, out.data());
+      for (uint64_t j = 0; j < m; j++) ns.images[(t * m + j) * 16 + b] = out[j];
+    }
+    in[t] = 0;
+  }
+}
+
+// The reconstruct of one erasure pattern (root.zig:268-335) as an n_in -> e map.
+// Inputs: every present original + the first e present recovery shards (exactly k:
+// the unique restored data does not depend on which k). Under D1 the literal
+// reconstruct is not a decoder, so its output depends on the pattern: keep ALL
+// present shards then, exactly as the reference would receive them.
+void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns) {
+  const bool d1 = flags & RS_FLAG_QUIRK_D1;
+  const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
+  uint64_t present_count = 0;
+  for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
+  const uint64_t want = d1 ? present_count : k;
+  std::vector<uint8_t> received(W, 0);
+  std::vector<uint64_t> in_pos, out_pos;
+  ns.src.clear();
+  for (uint64_t i = 0; i < k; i++)
+    if (present[i]) {
+      received[C + i] = 1;
+      in_pos.push_back(C + i);
+      ns.src.push_back(static_cast<int32_t>(i));
+    } else {
+      out_pos.push_back(C + i);
+    }
+  for (uint64_t r = 0; r < m && in_pos.size() < want; r++)
+    if (present[k + r]) {
+      received[r] = 1;
+      in_pos.push_back(r);
+      ns.src.push_back(kSrcRecovery | static_cast<int32_t>(r));
+    }
+  std::vector<uint16_t> er(kOrder);
+  erasure_logs(received.data(), k, m, er.data());
+  const size_t n_in = in_pos.size(), n_out = out_pos.size();
+  ns.n_in = static_cast<uint32_t>(n_in);
+  ns.n_out = static_cast<uint32_t>(n_out);
+  ns.images.assign(n_in * n_out * 16, 0);
+  std::vector<uint16_t> sym(W);
+  for (size_t t = 0; t < n_in; t++)
+    for (int b = 0; b < 16; b++) {  // images of basis symbol 1<<b at input t
+      std::fill(sym.begin(), sym.end(), 0);
+      sym[in_pos[t]] = static_cast<uint16_t>(1u << b);
+      scalar_reconstruct(sym.data(), received.data(), er.data(), k, m, d1);
+      for (size_t j = 0; j < n_out; j++) ns.images[(t * n_out + j) * 16 + b] = sym[out_pos[j]];
+    }
+}
+
 // root.zig:136-173 chunk schedule -> table block
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out) {
   char key[128];
@@ -148,16 +237,7 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   }
   const bool d1 = flags & RS_FLAG_QUIRK_D1, d2 = flags & RS_FLAG_QUIRK_D2;
   const uint64_t C = ceil_pow2(m);
-  std::vector<uint64_t> truncs;  // per IFFT chunk, chunk j at position j*C
-  truncs.push_back(std::min(k, C));
-  if (k > C) {
-    uint64_t cs = C;
-    while (d2 ? (cs + C < k) : (cs + C <= k)) {  // root.zig:151 (D2: `<`)
-      truncs.push_back(C);
-      cs += C;
-    }
-    if (k % C) truncs.push_back(k % C);  // root.zig:159-166
-  }
+  const std::vector<uint64_t> truncs = encode_chunk_truncs(k, m, d2);
   std::vector<RsTab> tabs;
   for (size_t j = 0; j < truncs.size(); j++) push_ifft_tabs(tabs, C, (j + 1) * C, d1);
   push_fft_tabs(tabs, C, 0, d1);
@@ -170,6 +250,9 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   plan->trunc_last = static_cast<uint32_t>(truncs.back());
   plan->tabs_per_chunk = static_cast<uint32_t>(ifft_tab_count(C));
   plan->work = static_cast<uint32_t>((k + C - 1) / C * C);
+  if (jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes)) {
+    encode_map(k, m, flags, plan->net->spec);
+  }
   g_enc_plans.emplace(key, plan);
   out = plan;
   return RS_OK;
@@ -230,7 +313,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
                     std::shared_ptr<DecodePlan> &out) {
   const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                    std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/";
+                    std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
+                    std::to_string(jit::enabled() && sb % jit::kUnitBytes == 0 && sb < (1ull << 32)) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::lock_guard<std::mutex> lk(g_plan_mu);
@@ -244,7 +328,13 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   uint64_t e = 0, present_count = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
-  const int kind = decode_kind(k, m, flags, e, present_count, sb);
+  int kind = decode_kind(k, m, flags, e, present_count, sb);
+  // bit-sliced network (rs_jit.hpp): the same e x k map as the matrix kernels at a
+  // fraction of their VALU cost, so preferred whenever it applies (modes auto / net)
+  const uint64_t n_in_want = d1 ? present_count : k;
+  const bool use_net = (mode == "auto" || mode == "net") && jit::enabled() &&
+                       jit::supports(static_cast<uint32_t>(n_in_want), static_cast<uint32_t>(e), sb);
+  if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
   const bool use_matrix = kind != 0;
 
   auto plan = std::make_shared<DecodePlan>();
@@ -253,40 +343,11 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   plan->trunc = static_cast<uint32_t>(end);
 
   if (use_matrix) {
-    // inputs: every present original + the first e present recovery shards (exactly k:
-    // the unique restored data does not depend on which k). Under D1 the literal
-    // reconstruct is not a decoder, so its output depends on the pattern: keep ALL
-    // present shards then, exactly as the reference would receive them.
-    const uint64_t want = d1 ? present_count : k;
-    std::vector<uint8_t> received(W, 0);
-    std::vector<uint64_t> in_pos, out_pos;
-    std::vector<int32_t> src;
-    for (uint64_t i = 0; i < k; i++)
-      if (present[i]) {
-        received[C + i] = 1;
-        in_pos.push_back(C + i);
-        src.push_back(static_cast<int32_t>(i));
-      } else {
-        out_pos.push_back(C + i);
-      }
-    for (uint64_t r = 0; r < m && in_pos.size() < want; r++)
-      if (present[k + r]) {
-        received[r] = 1;
-        in_pos.push_back(r);
-        src.push_back(kSrcRecovery | static_cast<int32_t>(r));
-      }
-    std::vector<uint16_t> er(kOrder);
-    erasure_logs(received.data(), k, m, er.data());
-    const size_t n_in = in_pos.size(), n_out = out_pos.size();
-    std::vector<uint16_t> img(n_in * n_out * 16);
-    std::vector<uint16_t> sym(W);
-    for (size_t t = 0; t < n_in; t++)
-      for (int b = 0; b < 16; b++) {  // images of basis symbol 1<<b at input t
-        std::fill(sym.begin(), sym.end(), 0);
-        sym[in_pos[t]] = static_cast<uint16_t>(1u << b);
-        scalar_reconstruct(sym.data(), received.data(), er.data(), k, m, d1);
-        for (size_t j = 0; j < n_out; j++) img[(t * n_out + j) * 16 + b] = sym[out_pos[j]];
-      }
+    jit::NetSpec map;
+    reconstruct_map(k, m, flags, present, map);
+    const std::vector<int32_t> &src = map.src;
+    const std::vector<uint16_t> &img = map.images;
+    const size_t n_in = map.n_in, n_out = map.n_out;
     // rows of n_out tables (kind 1) or padded to kMtileMaxOut zero tables (kind 2)
     const size_t row = kind == 2 ? kMtileMaxOut : n_out;
     std::vector<RsTab> tabs(n_in * row);
@@ -299,6 +360,10 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     if (st) return st;
     plan->matrix = true;
     plan->tiled = kind == 2;
+    if (use_net) {
+      plan->net = std::make_shared<NetSlot>();
+      plan->net->spec = std::move(map);
+    }
     plan->e = static_cast<uint32_t>(n_out);
     plan->n_in = static_cast<uint32_t>(n_in);
     plan->off_mat = 0;
@@ -471,7 +536,18 @@ const uint16_t *rs_table_log(void) { return tables().log; }
 const uint16_t *rs_table_skew(void) { return tables().skew; }
 const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
 
-const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) { return choose_encode(k, m, sb, 4).name; }
+// Names of the kernels a call with 16-byte aligned buffers would run (bit-sliced
+// networks: "net_i<inputs>_o<outputs>"; the hipRTC symbol adds a content hash).
+static const char *net_name(uint64_t n_in, uint64_t n_out) {
+  thread_local std::string name;
+  name = "net_i" + std::to_string(n_in) + "_o" + std::to_string(n_out);
+  return name.c_str();
+}
+
+const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
+  if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name(k, m);
+  return choose_encode(k, m, sb, 4).name;
+}
 const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const uint8_t *present) {
   std::vector<uint8_t> def;
   if (!present) {
@@ -482,11 +558,33 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   uint64_t e = 0, have = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
+  const std::string mode = decode_mode_env();
+  if ((mode == "auto" || mode == "net") && jit::enabled() &&
+      jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
+    return net_name(k, e);
   switch (decode_kind(k, m, flags_none(), e, have, sb)) {
     case 1: return choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name;
     case 2: return choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;
     default: return choose_decode(k, m, sb, 4).name;
   }
+}
+
+int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_t flags, double *compile_ms) {
+  int st = check_codec(k, m, jit::kUnitBytes);
+  if (st) return st;
+  jit::NetSpec spec;
+  if (present) {
+    uint64_t have = 0;
+    for (uint64_t i = 0; i < k + m; i++) have += present[i] != 0;
+    if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+    reconstruct_map(k, m, flags, present, spec);
+  } else {
+    encode_map(k, m, flags, spec);
+  }
+  if (!jit::supports(spec.n_in, spec.n_out, jit::kUnitBytes)) return fail(RS_ERR_INVALID_ARGUMENT, "no network form");
+  std::string err;
+  if (!jit::compile_check(spec, err, compile_ms, nullptr)) return fail(RS_ERR_DEVICE, err);
+  return RS_OK;
 }
 
 int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const void *d_original,
@@ -513,8 +611,16 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
   if ((st = current_device(&dev))) return st;
   std::shared_ptr<EncodePlan> plan;
   if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
-  const KernelChoice kc = choose_encode(k, m, sb, max_nv);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
+      jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
+    if (const jit::Kernel *nk = net_kernel(*plan->net)) {
+      HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
+                          static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));
+      return RS_OK;
+    }
+  }
+  const KernelChoice kc = choose_encode(k, m, sb, max_nv);
   EncodeArgs a{};
   a.data = static_cast<const uint8_t *>(d_original);
   a.data_stripe_stride = orig_stride;
@@ -591,6 +697,14 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   if ((st = current_device(&dev))) return st;
   std::shared_ptr<DecodePlan> plan;
   if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
+  if (plan->net && max_nv == 4) {
+    if (const jit::Kernel *nk = net_kernel(*plan->net)) {
+      HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,
+                          static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
+                          out_stride, sb, n_stripes, static_cast<hipStream_t>(stream)));
+      return RS_OK;
+    }
+  }
   const KernelChoice kc = plan->tiled    ? choose_decode_mtile(plan->e, sb, max_nv)
                           : plan->matrix ? choose_decode_matrix(plan->e, sb, max_nv)
                                          : choose_decode(k, m, sb, max_nv);

@@ -2,6 +2,7 @@
 // See rs_gf.hpp for the reference citations.
 #include "rs_gf.hpp"
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -193,6 +194,34 @@ void scalar_reconstruct(uint16_t *sym, const uint8_t *received, const uint16_t *
   scalar_fft(sym, W, end, 0, q);
   for (uint64_t i = C; i < end; i++)
     if (!received[i]) sym[i] = mul_engine(sym[i], static_cast<uint16_t>(kModulus - er[i]), q);
+}
+
+std::vector<uint64_t> encode_chunk_truncs(uint64_t k, uint64_t m, bool quirk_d2) {
+  const uint64_t C = ceil_pow2(m);
+  std::vector<uint64_t> truncs;  // chunk j at position j*C
+  truncs.push_back(std::min(k, C));
+  if (k > C) {
+    uint64_t cs = C;
+    while (quirk_d2 ? (cs + C < k) : (cs + C <= k)) {  // root.zig:151 (D2: `<`)
+      truncs.push_back(C);
+      cs += C;
+    }
+    if (k % C) truncs.push_back(k % C);  // root.zig:159-166
+  }
+  return truncs;
+}
+
+void scalar_encode(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, bool quirk_d2, uint16_t *out) {
+  const uint64_t C = ceil_pow2(m);
+  const std::vector<uint64_t> truncs = encode_chunk_truncs(k, m, quirk_d2);
+  std::vector<uint16_t> acc(C, 0), tmp(C);
+  for (size_t j = 0; j < truncs.size(); j++) {
+    for (uint64_t i = 0; i < C; i++) tmp[i] = j * C + i < k ? in[j * C + i] : 0;  // zero fill, root.zig:161
+    scalar_ifft(tmp.data(), C, truncs[j], (j + 1) * C, quirk_d1);  // root.zig:143-166
+    for (uint64_t i = 0; i < C; i++) acc[i] ^= tmp[i];
+  }
+  scalar_fft(acc.data(), C, m, 0, quirk_d1);  // root.zig:169
+  for (uint64_t i = 0; i < m; i++) out[i] = acc[i];
 }
 
 RsTab make_twiddle(uint32_t skew_index, bool quirk_d1) {

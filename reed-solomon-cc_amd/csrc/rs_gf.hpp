@@ -73,6 +73,11 @@ uint16_t mul_engine(uint16_t x, uint16_t log_m, bool quirk_d1);
 // pattern (root.zig:277-289), computed once by the caller.
 void scalar_reconstruct(uint16_t *sym, const uint8_t *received, const uint16_t *erasures, uint64_t k, uint64_t m,
                         bool quirk_d1);
+// Encoder.encode (root.zig:136-173) on one symbol per shard: in[k] -> out[m]
+// (used to derive the encode map for the bit-sliced network kernels).
+void scalar_encode(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, bool quirk_d2, uint16_t *out);
+// IFFT chunk truncations of the encode schedule (root.zig:143-166; D2 drops the last full chunk)
+std::vector<uint64_t> encode_chunk_truncs(uint64_t k, uint64_t m, bool quirk_d2);
 // root.zig:277-289: erasure flags for a received pattern -> evalPoly -> logs (65536 entries)
 void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *out);
 // Table for an FFT/IFFT twiddle: XOR-only marker when log_m == 65535

@@ -1,0 +1,394 @@
+// rs_jit.cpp — generator, hipRTC compiler and launcher of the bit-sliced
+// network kernels (rs_jit.hpp).
+#include "rs_jit.hpp"
+
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+
+#include "rs_internal.hpp"
+
+namespace rs {
+namespace jit {
+namespace {
+
+// Device-side helpers shared by every generated kernel.
+//  * ld / st: a wave covers 4 KiB of a shard = two 2 KiB regions of the
+//    contiguous lane layout of rs_device.hpp (lanes 0-31 read the lo halves,
+//    32-63 the hi halves of 16 consecutive 64-B chunks, 1 KiB per instruction),
+//    then one v_permlane32_swap per dword pairs every lane's lo and hi dwords.
+//    Lane result: lo[8] (lo bytes of 32 symbols) and hi[8] (their hi bytes).
+//  * tr8: in-place 8x8 bit transpose of every byte lane of x[0..8):
+//    afterwards bit b of byte q of x[j] = bit j of byte q of the input x[b],
+//    i.e. x[j] is bit-plane j of the 32 symbols (symbol of byte q of dword b at
+//    bit 8q+b, the same position in every plane). Three delta-swap stages of
+//    one shift + one v_bitop3 mux per word; an involution, so it also undoes
+//    itself on the way out.
+const char *kPrelude = R"HIP(
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef u32 v4 __attribute__((ext_vector_type(4)));
+#define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+#define MUX(a, b, m) __builtin_amdgcn_bitop3_b32((a), (b), (m), 0xE4)
+#define TRS(j, d, m)                 \
+  {                                  \
+    const u32 a = x[j], b = x[j + d]; \
+    x[j] = MUX(a, b << d, m);        \
+    x[j + d] = MUX(a >> d, b, m);    \
+  }
+__device__ __forceinline__ void tr8(u32 *x) {
+  TRS(0, 4, 0x0F0F0F0Fu) TRS(1, 4, 0x0F0F0F0Fu) TRS(2, 4, 0x0F0F0F0Fu) TRS(3, 4, 0x0F0F0F0Fu)
+  TRS(0, 2, 0x33333333u) TRS(1, 2, 0x33333333u) TRS(4, 2, 0x33333333u) TRS(5, 2, 0x33333333u)
+  TRS(0, 1, 0x55555555u) TRS(2, 1, 0x55555555u) TRS(4, 1, 0x55555555u) TRS(6, 1, 0x55555555u)
+}
+#if RS_NT
+#define LDV(p) __builtin_nontemporal_load((const v4 *)(p))
+#define STV(v, p) __builtin_nontemporal_store((v), (v4 *)(p))
+#else
+#define LDV(p) (*(const v4 *)(p))
+#define STV(v, p) (*(v4 *)(p) = (v))
+#endif
+struct Raw { v4 a0, a1, b0, b1; };
+__device__ __forceinline__ Raw ld(const unsigned char *p) {
+  Raw r;
+  r.a0 = LDV(p);
+  r.a1 = LDV(p + 1024);
+  r.b0 = LDV(p + 2048);
+  r.b1 = LDV(p + 3072);
+  return r;
+}
+__device__ __forceinline__ void planes(const Raw &r, u32 *P) {
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const auto s = __builtin_amdgcn_permlane32_swap(r.a0[v], r.a1[v], false, false);
+    const auto t = __builtin_amdgcn_permlane32_swap(r.b0[v], r.b1[v], false, false);
+    P[v] = s[0];
+    P[8 + v] = s[1];
+    P[4 + v] = t[0];
+    P[12 + v] = t[1];
+  }
+  tr8(P);
+  tr8(P + 8);
+}
+__device__ __forceinline__ void st(unsigned char *p, u32 *P) {
+  tr8(P);
+  tr8(P + 8);
+  v4 a0, a1, b0, b1;
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const auto s = __builtin_amdgcn_permlane32_swap(P[v], P[8 + v], false, false);
+    const auto t = __builtin_amdgcn_permlane32_swap(P[4 + v], P[12 + v], false, false);
+    a0[v] = s[0];
+    a1[v] = s[1];
+    b0[v] = t[0];
+    b1[v] = t[1];
+  }
+  STV(a0, p);
+  STV(a1, p + 1024);
+  STV(b0, p + 2048);
+  STV(b1, p + 3072);
+}
+)HIP";
+
+// XOR network of one input's 16 planes into up to 64 accumulator planes.
+// Four-Russians style: planes in groups of 4; per group every distinct nonzero
+// sub-row a row needs is built once (1 op each from the singles), then every
+// accumulator takes one XOR3 per pair of groups.
+void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::vector<bool> &init, int t) {
+  const size_t n = rows.size();
+  for (int pair = 0; pair < 2; pair++) {
+    std::string name[2][16];
+    for (int h = 0; h < 2; h++) {
+      const int g = 2 * pair + h;
+      bool need[16] = {};
+      for (size_t r = 0; r < n; r++) need[(rows[r] >> (4 * g)) & 15] = true;
+      auto single = [&](int i) { return "P[" + std::to_string(4 * g + i) + "]"; };
+      for (int i = 0; i < 4; i++) name[h][1 << i] = single(i);
+      // pairs first (so that 4-element combos can reuse one)
+      for (int msk = 1; msk < 16; msk++) {
+        const int pc = __builtin_popcount(msk);
+        if (!need[msk] || pc != 2) continue;
+        int b[2], nb = 0;
+        for (int i = 0; i < 4; i++)
+          if (msk >> i & 1) b[nb++] = i;
+        name[h][msk] = "c" + std::to_string(t) + "_" + std::to_string(g) + "_" + std::to_string(msk);
+        o << "  const u32 " << name[h][msk] << " = " << single(b[0]) << " ^ " << single(b[1]) << ";\n";
+      }
+      for (int msk = 1; msk < 16; msk++) {
+        const int pc = __builtin_popcount(msk);
+        if (!need[msk] || pc < 3) continue;
+        name[h][msk] = "c" + std::to_string(t) + "_" + std::to_string(g) + "_" + std::to_string(msk);
+        o << "  const u32 " << name[h][msk] << " = ";
+        if (pc == 3) {
+          int b[3], nb = 0;
+          for (int i = 0; i < 4; i++)
+            if (msk >> i & 1) b[nb++] = i;
+          o << "X3(" << single(b[0]) << ", " << single(b[1]) << ", " << single(b[2]) << ");\n";
+        } else {
+          static const int pairs[6][2] = {{3, 12}, {12, 3}, {5, 10}, {10, 5}, {6, 9}, {9, 6}};
+          bool done = false;
+          for (auto &pp : pairs)
+            if (!name[h][pp[0]].empty() && name[h][pp[0]][0] == 'c') {
+              const int r0 = __builtin_ctz(pp[1]), r1 = 31 - __builtin_clz(pp[1]);
+              o << "X3(" << name[h][pp[0]] << ", " << single(r0) << ", " << single(r1) << ");\n";
+              done = true;
+              break;
+            }
+          if (!done) o << "X3(" << single(0) << ", " << single(1) << ", " << single(2) << ") ^ " << single(3) << ";\n";
+        }
+      }
+    }
+    for (size_t r = 0; r < n; r++) {
+      std::string terms[2];
+      int nt = 0;
+      for (int h = 0; h < 2; h++) {
+        const int sub = (rows[r] >> (4 * (2 * pair + h))) & 15;
+        if (sub) terms[nt++] = name[h][sub];
+      }
+      if (!nt) continue;
+      const std::string acc = "a" + std::to_string(r);
+      if (!init[r]) {
+        o << "  " << acc << " = " << terms[0];
+        if (nt == 2) o << " ^ " << terms[1];
+        o << ";\n";
+        init[r] = true;
+      } else if (nt == 1) {
+        o << "  " << acc << " ^= " << terms[0] << ";\n";
+      } else {
+        o << "  " << acc << " = X3(" << acc << ", " << terms[0] << ", " << terms[1] << ");\n";
+      }
+    }
+  }
+}
+
+// Code-shape knobs (env, read at generation time; part of the cache key):
+//   RS_AMD_NET_PREFETCH  inputs loaded ahead of the one being transformed (default 0;
+//                        the compiler hoists the loads anyway)
+//   RS_AMD_NET_WAVES     amdgpu_waves_per_eu occupancy hint, 0 = none (default 0)
+//   RS_AMD_NET_NT        non-temporal loads/stores (default 1)
+struct Tuning {
+  int prefetch = 0, waves = 0, nt = 1;
+};
+
+int env_int(const char *name, int def) {
+  const char *e = std::getenv(name);
+  return e && *e ? std::atoi(e) : def;
+}
+
+Tuning tuning() {
+  Tuning t;
+  t.prefetch = std::max(0, std::min(8, env_int("RS_AMD_NET_PREFETCH", t.prefetch)));
+  t.waves = std::max(0, std::min(8, env_int("RS_AMD_NET_WAVES", t.waves)));
+  t.nt = env_int("RS_AMD_NET_NT", t.nt) != 0;
+  return t;
+}
+
+std::string tuning_key(const Tuning &t) {
+  return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt);
+}
+
+}  // namespace
+
+bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
+  return n_in > 0 && n_out > 0 && n_out <= kMaxOut && static_cast<uint64_t>(n_in) * n_out <= kMaxTerms &&
+         shard_bytes % kUnitBytes == 0 && shard_bytes < (1ull << 32);
+}
+
+std::string generate(const NetSpec &spec, const std::string &name) {
+  const uint32_t n_in = spec.n_in, n_out = spec.n_out;
+  const uint32_t n_tiles = (n_out + kTileOut - 1) / kTileOut;
+  const Tuning tu = tuning();
+  std::ostringstream o;
+  o << "#define RS_NT " << tu.nt << "\n" << kPrelude;
+  o << "extern \"C\" __global__ __launch_bounds__(256) ";
+  if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
+  o << "void " << name
+    << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
+       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0) {\n"
+       "  const u32 lane = threadIdx.x & 63;\n"
+    << "  const u32 tile = blockIdx.x % " << n_tiles << "u;\n"
+    << "  const u64 unit = (u64)(blockIdx.x / " << n_tiles << "u) * 4 + (threadIdx.x >> 6);\n"
+    << "  if (unit * 4096 >= sb) return;\n"
+       "  const u32 ll = lane & 31;\n"
+       "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n"
+       "  const u64 s = stripe0 + blockIdx.y;\n"
+       "  const unsigned char *B0 = b0 + s * s0;\n"
+       "  const unsigned char *B1 = b1 + s * s1;\n"
+       "  unsigned char *O = out + s * so;\n";
+  auto in_expr = [&](uint32_t t) {
+    const int32_t src = spec.src[t];
+    std::ostringstream e;
+    e << ((src & kSrcRecovery) ? "B1" : "B0") << " + " << (src & kSrcIndexMask) << "ull * sb + off";
+    return e.str();
+  };
+  for (uint32_t tile = 0; tile < n_tiles; tile++) {
+    const uint32_t j0 = tile * kTileOut, nj = std::min(kTileOut, n_out - j0);
+    const size_t n_acc = 16 * nj;
+    o << "  " << (tile ? "else if" : "if") << " (tile == " << tile << "u) {\n";
+    o << "  u32 ";
+    for (size_t r = 0; r < n_acc; r++) o << "a" << r << (r + 1 < n_acc ? ", " : ";\n");
+    std::vector<bool> init(n_acc, false);
+    // input t + prefetch is loaded just before input t is transformed
+    const uint32_t ahead = static_cast<uint32_t>(tu.prefetch);
+    for (uint32_t t = 0; t < n_in; t++) {
+      for (uint32_t u = t ? t + ahead : 0; u <= t + ahead && u < n_in; u++)
+        o << "  const Raw R" << u << " = ld(" << in_expr(u) << ");\n";
+      o << "  {\n";
+      o << "  u32 P[16];\n  planes(R" << t << ", P);\n";
+      std::vector<uint16_t> rows(n_acc, 0);
+      for (uint32_t jj = 0; jj < nj; jj++)
+        for (int b = 0; b < 16; b++) {
+          const uint16_t img = spec.images[(static_cast<size_t>(t) * n_out + j0 + jj) * 16 + b];
+          for (int c = 0; c < 16; c++)
+            if (img >> c & 1) rows[jj * 16 + c] |= static_cast<uint16_t>(1u << b);
+        }
+      emit_input(o, rows, init, static_cast<int>(t));
+      o << "  }\n";
+    }
+    for (size_t r = 0; r < n_acc; r++)
+      if (!init[r]) o << "  a" << r << " = 0u;\n";
+    for (uint32_t jj = 0; jj < nj; jj++) {
+      o << "  { u32 Q[16] = {";
+      for (int c = 0; c < 16; c++) o << "a" << jj * 16 + c << (c < 15 ? ", " : "};\n");
+      o << "    st(O + " << (j0 + jj) << "ull * sb + off, Q); }\n";
+    }
+    o << "  }\n";
+  }
+  o << "}\n";
+  return o.str();
+}
+
+// ------------------------------------------------------------- compile + cache
+namespace {
+
+std::mutex g_mu;
+std::map<std::string, std::unique_ptr<Kernel>> g_cache;  // key: device + spec bytes
+
+std::string spec_key(const NetSpec &s, int dev) {
+  std::string k = std::to_string(dev) + ":" + tuning_key(tuning()) + ":" + std::to_string(s.n_in) + ":" +
+                  std::to_string(s.n_out) + ":";
+  k.append(reinterpret_cast<const char *>(s.src.data()), s.src.size() * sizeof(int32_t));
+  k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
+  return k;
+}
+
+uint64_t fnv1a(const std::string &s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+std::string kernel_name(const NetSpec &spec, const std::string &key) {
+  char name[64];
+  std::snprintf(name, sizeof name, "rs_net_i%u_o%u_%016llx", spec.n_in, spec.n_out,
+                static_cast<unsigned long long>(fnv1a(key)));
+  return name;
+}
+
+// hipRTC: source -> gfx950 code object (needs no device)
+bool compile(const std::string &src, std::vector<char> &code, std::string &err) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rs_net.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+    return false;
+  }
+  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    err = std::string("hiprtcCompileProgram: ") + hiprtcGetErrorString(rc) + "\n" + log.substr(0, 2000);
+    hiprtcDestroyProgram(&prog);
+    return false;
+  }
+  size_t code_size = 0;
+  hiprtcGetCodeSize(prog, &code_size);
+  code.resize(code_size);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  return code_size > 0;
+}
+
+}  // namespace
+
+bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *code_bytes) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<char> code;
+  const bool ok = compile(generate(spec, kernel_name(spec, spec_key(spec, -1))), code, err);
+  if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (code_bytes) *code_bytes = code.size();
+  return ok;
+}
+
+bool enabled() {
+  const char *e = std::getenv("RS_AMD_JIT");
+  return !(e && std::strcmp(e, "0") == 0);
+}
+
+const Kernel *get(const NetSpec &spec, std::string &err) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    err = "hipGetDevice failed";
+    return nullptr;
+  }
+  const std::string key = spec_key(spec, dev);
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) return it->second.get();
+
+  const std::string name = kernel_name(spec, key);
+  const std::string src = generate(spec, name);
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<char> code;
+  if (!compile(src, code, err)) return nullptr;
+  auto k = std::make_unique<Kernel>();
+  hipError_t e = hipModuleLoadData(&k->module, code.data());
+  if (e != hipSuccess) {
+    err = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
+    return nullptr;
+  }
+  e = hipModuleGetFunction(&k->fn, k->module, name.c_str());
+  if (e != hipSuccess) {
+    err = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
+    return nullptr;
+  }
+  k->n_in = spec.n_in;
+  k->n_out = spec.n_out;
+  k->n_tiles = (spec.n_out + kTileOut - 1) / kTileOut;
+  k->name = name;
+  k->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (std::getenv("RS_AMD_JIT_VERBOSE"))
+    std::fprintf(stderr, "[rs_amd jit] %s compiled in %.0f ms (%zu B source, %zu B code)\n", name.c_str(),
+                 k->compile_ms, src.size(), code.size());
+  const Kernel *out = k.get();
+  g_cache.emplace(key, std::move(k));
+  return out;
+}
+
+hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const uint8_t *buf1, uint64_t stride1,
+                  uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s) {
+  const uint64_t units = shard_bytes / kUnitBytes;
+  const uint32_t gx = static_cast<uint32_t>((units + 3) / 4 * k.n_tiles);
+  for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
+    const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
+    const unsigned char *a0 = buf0, *a1 = buf1 ? buf1 : buf0;
+    unsigned char *o = out;
+    uint64_t st0 = stride0, st1 = buf1 ? stride1 : stride0, so = out_stride, sb = shard_bytes, first = s0;
+    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sb, &first};
+    hipError_t e = hipModuleLaunchKernel(k.fn, gx, gy, 1, 256, 1, 1, 0, s, args, nullptr);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace jit
+}  // namespace rs

@@ -1,0 +1,67 @@
+// rs_jit.hpp — bit-sliced GF(2)-linear network kernels, generated per plan and
+// compiled at plan time with hipRTC for gfx950.
+//
+// Both codec operations are, per 16-bit symbol position, GF(2)-linear maps from
+// the shards read to the shards written (encode: k data -> m parity,
+// root.zig:136-173; reconstruct for one erasure pattern: k received -> e
+// restored, root.zig:268-335; SURVEY.md §A.6 column independence). A plan turns
+// that map into a (16*n_out) x (16*n_in) GF(2) matrix and emits a kernel whose
+// lanes hold 32 symbols per shard as 16 bit-planes (one dword per bit position,
+// three delta-swap stages of a byte-lane 8x8 bit transpose on the way in and
+// out) and evaluate the matrix as a straight-line XOR network of v_bitop3_b32
+// (XOR3, full rate on gfx950). The matrix is a compile-time constant of the
+// generated source, so the network carries no table reads and no v_perm_b32
+// (half rate), which is what bounds the table-driven kernels in rs_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace rs {
+namespace jit {
+
+// One network: out[j] = XOR_t M_jt(in[t]) over n_in input shards.
+//   src[t]  : input shard t = (src & kSrcRecovery ? buffer 1 : buffer 0)[src & kSrcIndexMask]
+//   images  : images[(t * n_out + j) * 16 + b] = M_jt(1 << b) (16-bit symbol images)
+struct NetSpec {
+  uint32_t n_in = 0, n_out = 0;
+  std::vector<int32_t> src;
+  std::vector<uint16_t> images;
+};
+
+// Lanes cover 4 KiB of every shard per wave (32 symbols per lane): shard_bytes
+// must be a multiple of this, and below 4 GiB (32-bit lane offsets).
+constexpr uint64_t kUnitBytes = 4096;
+constexpr uint32_t kTileOut = 4;      // outputs per wave (64 accumulator planes)
+constexpr uint32_t kMaxOut = 16;      // tiles of kTileOut, one workgroup each
+constexpr uint64_t kMaxTerms = 4096;  // n_in * n_out cap (generated code size)
+
+bool enabled();  // RS_AMD_JIT != 0 and hipRTC usable
+bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
+
+// CUDA-style source of the kernel `name` (exposed for tests / inspection).
+std::string generate(const NetSpec &spec, const std::string &name);
+
+struct Kernel {
+  hipModule_t module = nullptr;
+  hipFunction_t fn = nullptr;
+  uint32_t n_in = 0, n_out = 0, n_tiles = 0;
+  std::string name;
+  double compile_ms = 0;
+};
+
+// Compiled kernel for `spec` on the current device (cached by content). Returns
+// nullptr and sets `err` when hipRTC is unavailable or compilation fails.
+const Kernel *get(const NetSpec &spec, std::string &err);
+
+// Generate and compile `spec` with hipRTC only (no device needed): a build check.
+bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *code_bytes);
+
+// buf0/buf1: input buffers ([stripe][shard][sb]); out: [stripe][n_out][sb].
+hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const uint8_t *buf1, uint64_t stride1,
+                  uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s);
+
+}  // namespace jit
+}  // namespace rs

@@ -83,6 +83,7 @@ def lib():
         "rs_reconstruct_batch_host": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32]),
         "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
         "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
+        "rs_net_compile_check": (C.c_int, [u64, u64, vp, u32, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_mul_scalar": (C.c_int, [vp, sz, C.c_uint16, u32]),
@@ -300,6 +301,15 @@ def reconstruct_kernel_name(k, m, shard_bytes, present=None) -> str:
         return lib().rs_reconstruct_kernel_name(k, m, shard_bytes, None).decode()
     pres = (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
     return lib().rs_reconstruct_kernel_name(k, m, shard_bytes, pres).decode()
+
+
+def net_compile_check(k, m, present=None, flags=0) -> float:
+    """Generate + hipRTC-compile the bit-sliced network of an encode (present None)
+    or of one reconstruct pattern, for gfx950, without a device. Returns ms."""
+    ms = C.c_double(0)
+    pres = None if present is None else (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
+    _check(lib().rs_net_compile_check(k, m, pres, flags, C.byref(ms)))
+    return ms.value
 
 
 # ------------------------------------------------------------ engine test shims

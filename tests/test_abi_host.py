@@ -112,10 +112,34 @@ def test_device_entry_points_fail_loudly_without_gpu():
         R.engine_mul_scalar(bytearray(64), 7)
 
 
-def test_kernel_selection():
+def test_kernel_selection_network():
+    """Bit-sliced network kernels (rs_jit.hpp) for shards in whole 4 KiB units and <= 16 outputs."""
+    assert R.encode_kernel_name(10, 4, 1 << 20) == "net_i10_o4"
+    assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "net_i10_o4"
+    assert R.encode_kernel_name(16, 16, 4096) == "net_i16_o16"
+    present = [1] * 20
+    present[3] = 0
+    assert R.reconstruct_kernel_name(16, 4, 8192, present) == "net_i16_o1"
+    assert R.encode_kernel_name(10, 4, 2048) == "encode_reg_w4_nv4"  # not a whole 4 KiB unit
+    assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"  # more than 16 outputs
+
+
+def test_kernel_selection(monkeypatch):
+    monkeypatch.setenv("RS_AMD_JIT", "0")
     assert R.encode_kernel_name(10, 4, 1 << 20) == "encode_reg_w4_nv4"
     assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "decode_matrix_e4_nv4"
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "decode_mtile16_nv1"
     assert R.reconstruct_kernel_name(200, 55, 320).startswith("decode_generic")
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"
     assert R.encode_kernel_name(100, 20, 1 << 18).startswith("encode_generic")
+
+
+def test_net_kernels_compile_for_gfx950():
+    """The generated bit-sliced network kernels (encode and one reconstruct pattern of
+    the bench shape, plus a quirk-mode encode) compile with hipRTC for gfx950 on a host
+    without a GPU: what a plan does before its first launch."""
+    assert R.net_compile_check(10, 4) > 0
+    assert R.net_compile_check(10, 4, [0, 0, 0, 0] + [1] * 10) > 0
+    assert R.net_compile_check(4, 2, None, 3) > 0
+    with pytest.raises(R.InvalidArgument):
+        R.net_compile_check(200, 55)  # 55 outputs: no network form

@@ -54,6 +54,13 @@ def nv(request, monkeypatch):
     return int(request.param)
 
 
+@pytest.fixture(params=["1", "0"])
+def jit(request, monkeypatch):
+    """RS_AMD_JIT: bit-sliced network kernels (hipRTC, rs_jit.hpp) on / off (table kernels)."""
+    monkeypatch.setenv("RS_AMD_JIT", request.param)
+    return request.param
+
+
 @pytest.fixture(params=["fft", "matrix", "auto"])
 def decode_mode(request, monkeypatch):
     """RS_AMD_DECODE: FFT kernels (root.zig:268-335 as written) or the e x k matrix kernel."""
@@ -147,8 +154,8 @@ KM_SMALL = [(1, 1), (2, 1), (4, 2), (3, 4), (5, 5), (10, 4), (8, 4), (12, 4), (6
 
 @pytest.mark.parametrize("k,m", KM_SMALL)
 @pytest.mark.parametrize("flags", [0, 3])
-@pytest.mark.parametrize("sb", [320, 4096])  # 4096: whole 2 KiB waves -> contiguous layout, ws64 path
-def test_encode_vs_oracle(oracle, nv, k, m, flags, sb):
+@pytest.mark.parametrize("sb", [320, 4096])  # 4096: whole 4 KiB waves -> network / contiguous layout, ws64 path
+def test_encode_vs_oracle(oracle, nv, jit, k, m, flags, sb):
     rng = np.random.default_rng(k * 7919 + m * 31 + flags)
     n = 3
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
@@ -178,6 +185,68 @@ def test_reconstruct_vs_oracle(oracle, nv, decode_mode, k, m, sb):
         # and the oracle agrees with itself through the same API
         exp = oracle.reconstruct_batch(k, m, present, np.concatenate([data, par], axis=1))
         assert (got == exp).all()
+
+
+# ------------------------------------------------- bit-sliced network kernels
+NET_KM = [(1, 1), (2, 1), (4, 2), (3, 4), (5, 5), (10, 4), (8, 4), (12, 4), (6, 3), (9, 8), (16, 16), (17, 16),
+          (20, 16), (16, 8), (30, 2), (64, 4), (100, 8), (13, 7)]
+
+
+@pytest.mark.parametrize("k,m", NET_KM)
+@pytest.mark.parametrize("flags", [0, 1, 3])
+def test_net_reconstruct_vs_oracle(oracle, monkeypatch, k, m, flags):
+    """RS_AMD_DECODE=net: the e x k reconstruct map as a generated XOR network,
+    against the oracle (both quirk modes: the D1 multiply is GF(2)-linear too)."""
+    if not R.use_high_rate(k, m):
+        pytest.skip("low rate")
+    monkeypatch.setenv("RS_AMD_DECODE", "net")
+    rng = np.random.default_rng(k * 131 + m * 7 + flags)
+    sb, n = 8192, 2
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags)
+    shards = np.concatenate([data, par], axis=1)
+    for trial in range(2):
+        e = int(rng.integers(1, min(k, m) + 1))
+        lost = list(rng.choice(k, size=e, replace=False))
+        extra = int(rng.integers(0, m - e + 1))  # also drop some recovery shards
+        lost += [k + int(i) for i in rng.choice(m, size=extra, replace=False)]
+        present = np.ones(k + m, np.uint8)
+        present[lost] = 0
+        missing = [i for i in range(k) if not present[i]]
+        name = R.reconstruct_kernel_name(k, m, sb, present)
+        got = gpu_reconstruct(k, m, present, data, par, flags)
+        exp = oracle.reconstruct_batch(k, m, present, shards, quirks=flags)
+        assert (got == exp).all(), (k, m, flags, lost, name)
+        if flags & 1 == 0:
+            assert (got == data[:, missing]).all()
+
+
+@pytest.mark.parametrize("k,m,sb", [(10, 4, 4096), (10, 4, 12288), (16, 16, 4096), (4, 2, 65536), (30, 2, 8192)])
+def test_net_matches_table_kernels(monkeypatch, k, m, sb):
+    """Network kernels == table-driven kernels (JIT on/off), encode and reconstruct,
+    on padded (strided) stripes."""
+    rng = np.random.default_rng(sb + k)
+    n = 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    present = np.ones(k + m, np.uint8)
+    present[rng.choice(k, size=min(k, m), replace=False)] = 0
+    missing = [i for i in range(k) if not present[i]]
+    outs = {}
+    for j in ("1", "0"):
+        monkeypatch.setenv("RS_AMD_JIT", j)
+        big = torch.zeros((n, k * sb + 4096), dtype=torch.uint8, device=DEV)  # stripe stride > k*sb
+        big[:, :k * sb] = to_dev(data.reshape(n, -1))
+        par = torch.zeros((n, m * sb + 1024), dtype=torch.uint8, device=DEV)
+        assert R.lib().rs_encode_batch_dev(k, m, sb, n, big.data_ptr(), big.stride(0), par.data_ptr(),
+                                           par.stride(0), 0, None) == 0, R.lib().rs_last_error()
+        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8, device=DEV)
+        assert R.lib().rs_reconstruct_batch_dev(k, m, sb, n, present.ctypes.data, big.data_ptr(), big.stride(0),
+                                                par.data_ptr(), par.stride(0), out.data_ptr(), out.stride(0),
+                                                0, None) == 0, R.lib().rs_last_error()
+        torch.cuda.synchronize()
+        outs[j] = par[:, :m * sb].cpu().numpy()
+        assert (out.cpu().numpy() == data[:, missing]).all(), j
+    assert (outs["1"] == outs["0"]).all()
 
 
 def test_reconstruct_not_enough_shards():
