@@ -159,10 +159,10 @@ int rs_reconstruct_batch_host(uint64_t original_count, uint64_t recovery_count, 
                               uint64_t recovery_stripe_stride, void *h_restored, uint64_t restored_stripe_stride,
                               uint32_t flags);
 
-/* Which device kernel a call would run on ("net_i10_o4", "encode_reg_w4_nv4",
+/* Which device kernel a call would run on ("net_encode_i10_o4", "encode_reg_w4_nv4",
  * "decode_matrix_e4_nv4", "encode_generic_nv1", ...), assuming 16-byte aligned buffers.
  * present: k+m flags as for rs_reconstruct_batch_dev, or NULL for "the first min(k, m)
- * originals lost". net_* = bit-sliced XOR network generated for the plan and compiled
+ * originals lost". net_<role>_* = bit-sliced XOR network generated for the plan and compiled
  * with hipRTC on first use (shard_bytes a multiple of 4096, <= 16 outputs; disable
  * with RS_AMD_JIT=0). */
 const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);

@@ -165,6 +165,7 @@ int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out
 // symbol of every data shard through Encoder.encode (root.zig:136-173).
 void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
   const bool d1 = flags & RS_FLAG_QUIRK_D1, d2 = flags & RS_FLAG_QUIRK_D2;
+  ns.role = "encode";
   ns.n_in = static_cast<uint32_t>(k);
   ns.n_out = static_cast<uint32_t>(m);
   ns.src.clear();
@@ -194,6 +195,7 @@ void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *pres
   const uint64_t want = d1 ? present_count : k;
   std::vector<uint8_t> received(W, 0);
   std::vector<uint64_t> in_pos, out_pos;
+  ns.role = "reconstruct";
   ns.src.clear();
   for (uint64_t i = 0; i < k; i++)
     if (present[i]) {
@@ -537,15 +539,15 @@ const uint16_t *rs_table_skew(void) { return tables().skew; }
 const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
 
 // Names of the kernels a call with 16-byte aligned buffers would run (bit-sliced
-// networks: "net_i<inputs>_o<outputs>"; the hipRTC symbol adds a content hash).
-static const char *net_name(uint64_t n_in, uint64_t n_out) {
+// networks: "net_<role>_i<inputs>_o<outputs>"; the hipRTC symbol rs_net_... adds a content hash).
+static const char *net_name(const char *role, uint64_t n_in, uint64_t n_out) {
   thread_local std::string name;
-  name = "net_i" + std::to_string(n_in) + "_o" + std::to_string(n_out);
+  name = std::string("net_") + role + "_i" + std::to_string(n_in) + "_o" + std::to_string(n_out);
   return name.c_str();
 }
 
 const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
-  if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name(k, m);
+  if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name("encode", k, m);
   return choose_encode(k, m, sb, 4).name;
 }
 const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const uint8_t *present) {
@@ -561,7 +563,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   const std::string mode = decode_mode_env();
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
-    return net_name(k, e);
+    return net_name("reconstruct", k, e);
   switch (decode_kind(k, m, flags_none(), e, have, sb)) {
     case 1: return choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name;
     case 2: return choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;

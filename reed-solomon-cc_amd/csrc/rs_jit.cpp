@@ -272,7 +272,7 @@ std::mutex g_mu;
 std::map<std::string, std::unique_ptr<Kernel>> g_cache;  // key: device + spec bytes
 
 std::string spec_key(const NetSpec &s, int dev) {
-  std::string k = std::to_string(dev) + ":" + tuning_key(tuning()) + ":" + std::to_string(s.n_in) + ":" +
+  std::string k = std::to_string(dev) + ":" + s.role + ":" + tuning_key(tuning()) + ":" + std::to_string(s.n_in) + ":" +
                   std::to_string(s.n_out) + ":";
   k.append(reinterpret_cast<const char *>(s.src.data()), s.src.size() * sizeof(int32_t));
   k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
@@ -286,8 +286,8 @@ uint64_t fnv1a(const std::string &s) {
 }
 
 std::string kernel_name(const NetSpec &spec, const std::string &key) {
-  char name[64];
-  std::snprintf(name, sizeof name, "rs_net_i%u_o%u_%016llx", spec.n_in, spec.n_out,
+  char name[96];
+  std::snprintf(name, sizeof name, "rs_net_%s_i%u_o%u_%016llx", spec.role.c_str(), spec.n_in, spec.n_out,
                 static_cast<unsigned long long>(fnv1a(key)));
   return name;
 }

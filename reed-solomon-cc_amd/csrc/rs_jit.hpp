@@ -26,6 +26,7 @@ namespace jit {
 //   src[t]  : input shard t = (src & kSrcRecovery ? buffer 1 : buffer 0)[src & kSrcIndexMask]
 //   images  : images[(t * n_out + j) * 16 + b] = M_jt(1 << b) (16-bit symbol images)
 struct NetSpec {
+  std::string role = "net";  // "encode" / "reconstruct": kernel symbol rs_net_<role>_i<n_in>_o<n_out>_<hash>
   uint32_t n_in = 0, n_out = 0;
   std::vector<int32_t> src;
   std::vector<uint16_t> images;

@@ -114,12 +114,12 @@ def test_device_entry_points_fail_loudly_without_gpu():
 
 def test_kernel_selection_network():
     """Bit-sliced network kernels (rs_jit.hpp) for shards in whole 4 KiB units and <= 16 outputs."""
-    assert R.encode_kernel_name(10, 4, 1 << 20) == "net_i10_o4"
-    assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "net_i10_o4"
-    assert R.encode_kernel_name(16, 16, 4096) == "net_i16_o16"
+    assert R.encode_kernel_name(10, 4, 1 << 20) == "net_encode_i10_o4"
+    assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "net_reconstruct_i10_o4"
+    assert R.encode_kernel_name(16, 16, 4096) == "net_encode_i16_o16"
     present = [1] * 20
     present[3] = 0
-    assert R.reconstruct_kernel_name(16, 4, 8192, present) == "net_i16_o1"
+    assert R.reconstruct_kernel_name(16, 4, 8192, present) == "net_reconstruct_i16_o1"
     assert R.encode_kernel_name(10, 4, 2048) == "encode_reg_w4_nv4"  # not a whole 4 KiB unit
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"  # more than 16 outputs
 

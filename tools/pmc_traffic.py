@@ -17,6 +17,9 @@ import statistics
 
 
 def short_name(full):
+    m = re.search(r"rs_net_(encode|reconstruct)_i(\d+)_o(\d+)_[0-9a-f]+", full)
+    if m:
+        return f"net_{m.group(1)}_i{m.group(2)}_o{m.group(3)}"
     m = re.search(r"k_(encode_reg|decode_reg|decode_matrix)<(\d+), (\d+)>", full)
     if m:
         kind, size, nv = m.groups()
@@ -55,7 +58,7 @@ def main():
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
     for n in sorted(set(fetch) & set(write)):
         f, w = 2.0 * fetch[n], write[n]
-        alg = ((a.k + a.m) if n.startswith("encode") else (a.k + a.e)) * a.shard_bytes
+        alg = ((a.k + a.m) if n.startswith(("encode", "net_encode")) else (a.k + a.e)) * a.shard_bytes
         out[n] = {"fetch_bytes_per_stripe": f / a.stripes, "write_bytes_per_stripe": w / a.stripes,
                   "hbm_bytes_per_stripe": (f + w) / a.stripes, "algorithmic_bytes_per_stripe": alg,
                   "traffic_over_algorithmic": round((f + w) / a.stripes / alg, 4),
