@@ -37,7 +37,9 @@ struct NetSpec {
 constexpr uint64_t kUnitBytes = 4096;
 constexpr uint32_t kTileOut = 4;      // outputs per wave (64 accumulator planes)
 constexpr uint32_t kMaxOut = 16;      // tiles of kTileOut, one workgroup each
-constexpr uint64_t kMaxTerms = 4096;  // n_in * n_out cap (generated code size)
+// generated code size: n_in x tiles input blocks of ~270 instructions each; hipRTC
+// takes ~20-40 ms per block, so the cap keeps a plan's compile near 1-2 s
+constexpr uint64_t kMaxBlocks = 64;
 
 bool enabled();  // RS_AMD_JIT != 0 and hipRTC usable
 bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
