@@ -131,6 +131,10 @@ struct DecodePlan {
   uint32_t work = 0, chunk = 0, trunc = 0, e = 0, n_in = 0;
   size_t off_fft = 0, off_pre = 0, off_post = 0, off_src = 0, off_dst = 0, off_mat = 0;  // byte offsets into buf
   std::shared_ptr<NetSlot> net;  // set when the pattern runs as a bit-sliced network
+  // reconstruct by syndromes: encode the received data (erased shards skipped) into
+  // a scratch, then the e x e matrix kernel on rec ^ scratch rows (see syndrome_map)
+  bool syndrome = false;
+  std::shared_ptr<DevBuf> skip;  // k-bit mask of the erased data shards
 };
 
 // Compile (once) and return the plan's network kernel; nullptr if hipRTC failed
@@ -309,6 +313,98 @@ int decode_kind(uint64_t k, uint64_t m, uint32_t flags, uint64_t e, uint64_t pre
   return small_ok ? 1 : tiled_ok ? 2 : 0;
 }
 
+// Multiplies of one encode (root.zig:136-173) per 64-B column (live twiddles only).
+uint64_t fft_encode_mul_count(uint64_t k, uint64_t m) {
+  const uint64_t C = ceil_pow2(m);
+  const uint16_t *sk = tables().skew;
+  auto live = [&](uint64_t idx) -> uint64_t { return idx < kModulus && sk[idx] != kModulus ? 1 : 0; };
+  auto group = [&](uint64_t b, uint64_t d) { return d * (live(b) + live(b + 2 * d)) + 2 * d * live(b + d); };
+  const std::vector<uint64_t> truncs = encode_chunk_truncs(k, m, false);
+  uint64_t n = 0;
+  for (size_t j = 0; j < truncs.size(); j++) {  // IFFT per chunk, Generic.zig:80-147
+    const uint64_t sd = (j + 1) * C;
+    uint64_t d = 1;
+    for (uint64_t d4 = 4; d4 <= C; d = d4, d4 <<= 2)
+      for (uint64_t r = 0; r < truncs[j]; r += d4) n += group(r + d + sd - 1, d);
+    if (d < C) n += d * live(d + sd - 1);
+  }
+  uint64_t d4 = C;  // FFT, Generic.zig:15-78
+  for (uint64_t dd = C >> 2; dd != 0; d4 = dd, dd >>= 2)
+    for (uint64_t r = 0; r < m; r += d4) n += group(r + dd - 1, dd);
+  if (d4 == 2)
+    for (uint64_t r = 0; r < m; r += 2) n += live(r);
+  return n;
+}
+
+// Reconstruct by syndromes instead of the k x e matrix: worth it for wide codes
+// with many erasures (RS(200,55) losing 55: 785 + 0.75*55^2 multiplies per column
+// against 0.75*200*55). Needs the corrected multiply (under D1 the literal
+// reconstruct is no inverse of the encode) and a fused (non-generic) encode kernel.
+bool syndrome_pick(uint64_t k, uint64_t m, uint64_t e, uint32_t flags, uint64_t sb, const std::string &mode) {
+  if ((flags & RS_FLAG_QUIRK_D1) || e == 0 || e > kMtileMaxOut || sb % 512) return false;
+  if (choose_encode(k, m, sb, 4).variant == Variant::kGeneric) return false;
+  if (mode == "syndrome") return true;
+  if (mode != "auto") return false;
+  const double direct = 0.75 * static_cast<double>(k) * e;
+  const double syn = static_cast<double>(fft_encode_mul_count(k, m)) + 0.75 * static_cast<double>(e) * e;
+  return syn < 0.7 * direct;
+}
+
+// x = A^-1 (p_R ^ Enc_R(d')): R = the first e received recovery rows, d' = the
+// received data with the erased shards zeroed, A = the encode map from the erased
+// columns to the rows R (e x e blocks of 16x16 GF(2) maps, invertible: the code is
+// MDS). A is inverted as a 16e x 16e GF(2) matrix; the result is a matrix-kernel
+// map whose input i is the syndrome rec[R_i] ^ Enc(d')[R_i] (kSrcXorScratch).
+int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &ns) {
+  std::vector<uint64_t> E, Rr;
+  for (uint64_t i = 0; i < k; i++)
+    if (!present[i]) E.push_back(i);
+  for (uint64_t r = 0; r < m && Rr.size() < E.size(); r++)
+    if (present[k + r]) Rr.push_back(r);
+  const size_t e = E.size();
+  if (Rr.size() < e) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+  const size_t N = 16 * e, words = (2 * N + 63) / 64;
+  // augmented [A | I], row (16 j + c) = bit c of the row-R_j output, column (16 t + b) = basis b of column E_t
+  std::vector<std::vector<uint64_t>> M(N, std::vector<uint64_t>(words, 0));
+  std::vector<uint16_t> in(k, 0), out(m);
+  for (size_t t = 0; t < e; t++)
+    for (int b = 0; b < 16; b++) {
+      in[E[t]] = static_cast<uint16_t>(1u << b);
+      scalar_encode(in.data(), k, m, false, false, out.data());
+      in[E[t]] = 0;
+      const size_t col = 16 * t + b;
+      for (size_t j = 0; j < e; j++)
+        for (int c = 0; c < 16; c++)
+          if (out[Rr[j]] >> c & 1) M[16 * j + c][col / 64] |= 1ull << (col % 64);
+    }
+  for (size_t r = 0; r < N; r++) M[r][(N + r) / 64] |= 1ull << ((N + r) % 64);
+  for (size_t col = 0; col < N; col++) {  // Gauss-Jordan over GF(2)
+    size_t piv = col;
+    while (piv < N && !(M[piv][col / 64] >> (col % 64) & 1)) piv++;
+    if (piv == N) return fail(RS_ERR_DEVICE, "syndrome matrix singular");
+    std::swap(M[piv], M[col]);
+    for (size_t r = 0; r < N; r++)
+      if (r != col && (M[r][col / 64] >> (col % 64) & 1))
+        for (size_t w = 0; w < words; w++) M[r][w] ^= M[col][w];
+  }
+  // B = A^-1: x bit (16 j + c) = XOR over s bits (16 i + b) of B[16 j + c][16 i + b]
+  ns.role = "syndrome";
+  ns.n_in = static_cast<uint32_t>(e);
+  ns.n_out = static_cast<uint32_t>(e);
+  ns.src.assign(e, 0);
+  ns.images.assign(e * e * 16, 0);
+  for (size_t i = 0; i < e; i++) {
+    ns.src[i] = kSrcXorScratch | kSrcRecovery | static_cast<int32_t>(Rr[i]);
+    for (int b = 0; b < 16; b++) {
+      const size_t col = N + 16 * i + b;
+      for (size_t j = 0; j < e; j++)
+        for (int c = 0; c < 16; c++)
+          if (M[16 * j + c][col / 64] >> (col % 64) & 1) ns.images[(i * e + j) * 16 + b] |= static_cast<uint16_t>(1u << c);
+    }
+  }
+  return RS_OK;
+}
+
 // root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
 // kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
@@ -337,6 +433,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   const bool use_net = (mode == "auto" || mode == "net") && jit::enabled() &&
                        jit::supports(static_cast<uint32_t>(n_in_want), static_cast<uint32_t>(e), sb);
   if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
+  const bool use_syn = !use_net && syndrome_pick(k, m, e, flags, sb, mode);
+  if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
   const bool use_matrix = kind != 0;
 
   auto plan = std::make_shared<DecodePlan>();
@@ -346,7 +444,17 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
 
   if (use_matrix) {
     jit::NetSpec map;
-    reconstruct_map(k, m, flags, present, map);
+    if (use_syn) {
+      int st = syndrome_map(k, m, present, map);
+      if (st) return st;
+      std::vector<uint32_t> bits((k + 31) / 32, 0);
+      for (uint64_t i = 0; i < k; i++)
+        if (!present[i]) bits[i / 32] |= 1u << (i % 32);
+      if ((st = upload(bits.data(), bits.size() * sizeof(uint32_t), dev, plan->skip))) return st;
+      plan->syndrome = true;
+    } else {
+      reconstruct_map(k, m, flags, present, map);
+    }
     const std::vector<int32_t> &src = map.src;
     const std::vector<uint16_t> &img = map.images;
     const size_t n_in = map.n_in, n_out = map.n_out;
@@ -564,6 +672,13 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
     return net_name("reconstruct", k, e);
+  if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
+    thread_local std::string name;
+    name = std::string("syndrome+") + choose_encode(k, m, sb, 4).name + "+" +
+           (e <= kMatrixMaxOut ? choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name
+                               : choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name);
+    return name.c_str();
+  }
   switch (decode_kind(k, m, flags_none(), e, have, sb)) {
     case 1: return choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name;
     case 2: return choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;
@@ -734,6 +849,54 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
   if (!a.orig) a.orig = a.rec;  // never dereferenced for absent shards
   if (!a.rec) a.rec = a.orig;
+  if (plan->syndrome) {
+    // 1) Enc(d') of the received data (erased shards skipped) into a scratch,
+    // 2) the e x e matrix kernel on the syndromes rec[R_i] ^ scratch[R_i]
+    std::shared_ptr<EncodePlan> ep;
+    if ((st = get_encode_plan(dev, k, m, RS_FLAG_CORRECTED, ep))) return st;
+    const KernelChoice ke = choose_encode(k, m, sb, max_nv);
+    EncodeArgs ea{};
+    ea.data = a.orig;
+    ea.data_stripe_stride = orig_stride;
+    ea.parity_stripe_stride = m * sb;
+    ea.shard_bytes = sb;
+    ea.tabs = static_cast<const RsTab *>(ep->buf->p);
+    ea.chunk = ep->chunk;
+    ea.n_chunks = ep->n_chunks;
+    ea.trunc_first = ep->trunc_first;
+    ea.trunc_last = ep->trunc_last;
+    ea.m = static_cast<uint32_t>(m);
+    ea.k = static_cast<uint32_t>(k);
+    ea.tabs_per_chunk = ep->tabs_per_chunk;
+    ea.work = ep->work;
+    ea.contig = contig_ok(sb, ke.nv);
+    ea.skip = static_cast<const uint32_t *>(plan->skip->p);
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap * 4 / (m * sb)));
+    void *scratch = nullptr;
+    HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));
+    for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
+      const uint64_t cnt = std::min(per, n_stripes - s0);
+      EncodeArgs eb = ea;
+      eb.data += s0 * orig_stride;
+      eb.parity = static_cast<uint8_t *>(scratch);
+      eb.n_stripes = cnt;
+      DecodeArgs db = a;
+      db.orig += s0 * orig_stride;
+      db.rec += s0 * rec_stride;
+      db.out += s0 * out_stride;
+      db.xsrc = static_cast<const uint8_t *>(scratch);
+      db.xsrc_stripe_stride = m * sb;
+      db.n_stripes = cnt;
+      hipError_t err = launch_encode(ke, eb, s);
+      if (err == hipSuccess) err = launch_decode(kc, db, s);
+      if (err != hipSuccess) {
+        (void)hipFreeAsync(scratch, s);
+        return hip_fail(err, "syndrome reconstruct");
+      }
+    }
+    HIP_TRY(hipFreeAsync(scratch, s));
+    return RS_OK;
+  }
   if (kc.variant != Variant::kGeneric) {
     a.n_stripes = n_stripes;
     HIP_TRY(launch_decode(kc, a, s));

@@ -30,6 +30,7 @@ struct EncodeArgs {
   uint8_t *scratch;      // generic path only: [stripe][Wenc][sb]
   uint64_t scratch_stripes;
   bool contig;           // lane layout (dev::load_sym): contiguous waves vs split halves
+  const uint32_t *skip = nullptr;  // device bitmask of k bits: data shards read as zero (syndrome reconstruct)
 };
 
 // Reconstruct: positions per root.zig:199-229 (recovery at [0,m), originals at
@@ -66,7 +67,12 @@ struct DecodeArgs {
   // per-stripe patterns: tab_pre/tab_post/pos_src/pos_dst advance by
   // s * pattern_stride entries for stripe s (0 = one plan for the batch)
   uint64_t pattern_stride;
+  // syndrome reconstruct: an input flagged kSrcXorScratch is rec[idx] ^ xsrc[idx]
+  // (xsrc = the encode of the received data, [stripe][m][shard_bytes])
+  const uint8_t *xsrc = nullptr;
+  uint64_t xsrc_stripe_stride = 0;
 };
+constexpr int32_t kSrcXorScratch = 0x20000000;
 constexpr int32_t kSrcRecovery = 0x40000000;
 constexpr int32_t kSrcIndexMask = 0x00FFFFFF;
 

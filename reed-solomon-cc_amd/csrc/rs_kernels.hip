@@ -50,6 +50,13 @@ __device__ __forceinline__ bool lane_offset(uint64_t shard_bytes, bool contig, u
   return true;
 }
 
+// Encode of a partial data set (reconstruct by syndromes, rs_capi.cpp): data
+// shard `idx` flagged in the skip bitmask is read as zeros (never touched).
+__device__ __forceinline__ bool skipped(const EncodeArgs &a, uint32_t idx) {
+  typedef const __attribute__((address_space(4))) uint32_t *CU;
+  return a.skip && ((((CU)(a.skip))[idx >> 5] >> (idx & 31)) & 1u);
+}
+
 // ============================================================ fused encode
 template <int C, int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
@@ -64,7 +71,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
     // first chunk: root.zig:143-146
 #pragma unroll
     for (int p = 0; p < C; p++) {
-      if (static_cast<uint32_t>(p) < a.trunc_first) dev::load_sym(acc[p], src + p * sb, off, a.contig);
+      if (static_cast<uint32_t>(p) < a.trunc_first && !skipped(a, p))
+        dev::load_sym(acc[p], src + p * sb, off, a.contig);
       else dev::zero(acc[p]);
     }
     dev::ifft_regs<C>(acc, a.tabs, a.trunc_first);
@@ -75,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
       Sym<NV> cur[C];
 #pragma unroll
       for (int p = 0; p < C; p++) {
-        if (static_cast<uint32_t>(p) < t) dev::load_sym(cur[p], cs + p * sb, off, a.contig);
+        if (static_cast<uint32_t>(p) < t && !skipped(a, j * C + p)) dev::load_sym(cur[p], cs + p * sb, off, a.contig);
         else dev::zero(cur[p]);
       }
       const RsTab *tj = a.tabs + j * TI;
@@ -207,7 +215,37 @@ __device__ __forceinline__ void fft4(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Four radix-4 groups that share one twiddle triple (stages d=4 and d=16 of a
+// wave's layout): the three tables are loaded once for the four quads.
 template <int NV>
+__device__ __forceinline__ void ifft4x4(Sym<NV> *c, const RsTab *g) {
+  __builtin_amdgcn_sched_barrier(0);
+  const Tab m01 = dev::load_tab(g), m23 = dev::load_tab(g + 2), m02 = dev::load_tab(g + 1);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    dev::ifft_bf(c[i], c[i + 4], m01);
+    dev::ifft_bf(c[i + 8], c[i + 12], m23);
+    dev::ifft_bf(c[i], c[i + 8], m02);
+    dev::ifft_bf(c[i + 4], c[i + 12], m02);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NV>
+__device__ __forceinline__ void fft4x4(Sym<NV> *c, const RsTab *g) {
+  __builtin_amdgcn_sched_barrier(0);
+  const Tab m02 = dev::load_tab(g + 1), m01 = dev::load_tab(g), m23 = dev::load_tab(g + 2);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    dev::fft_bf(c[i], c[i + 8], m02);
+    dev::fft_bf(c[i + 4], c[i + 12], m02);
+    dev::fft_bf(c[i], c[i + 4], m01);
+    dev::fft_bf(c[i + 8], c[i + 12], m23);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int NV, bool SHARED>
 __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
   constexpr int TI = 63;  // ifft_tab_count(64): 16 + 4 + 1 groups x 3
   __shared__ LdsSym<NV> lds[64][64];
@@ -231,7 +269,8 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
 #pragma unroll
       for (int j = 0; j < 16; j++) {  // layout A
         const uint32_t pos = 16 * w + j;
-        if (pos < t) dev::load_sym(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
+        if (pos < t && !skipped(a, c * 64 + pos))
+          dev::load_sym(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
         else dev::zero(cur[j]);
       }
 #pragma unroll
@@ -240,8 +279,12 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
         if (r < t) ifft4(cur[4 * g], cur[4 * g + 1], cur[4 * g + 2], cur[4 * g + 3], tc + r / 4 * 3);
       }
       if (16 * w < t) {  // stage d=4, group r = 16w
+        if constexpr (SHARED) {
+          ifft4x4(cur, tc + 48 + w * 3);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 48 + w * 3);
+          for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 48 + w * 3);
+        }
       }
       __syncthreads();  // previous readers of lds are done
 #pragma unroll
@@ -249,15 +292,23 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < 16; u++) lds_get(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, cur[u]);  // layout B
+      if constexpr (SHARED) {
+        ifft4x4(cur, tc + 60);  // d=16
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 60);  // d=16
+        for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 60);  // d=16
+      }
 #pragma unroll
       for (int u = 0; u < 16; u++) dev::xor_into(acc[u], cur[u]);  // root.zig:153-155
     }
     // FFT(0, 64, trunc m) on acc, root.zig:169
     const RsTab *tf = a.tabs + a.n_chunks * TI;
+    if constexpr (SHARED) {
+      fft4x4(acc, tf);  // d=16 (layout B)
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf);  // d=16 (layout B)
+      for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf);  // d=16 (layout B)
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 16; u++) lds_put(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, acc[u]);
@@ -265,8 +316,12 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
 #pragma unroll
     for (int j = 0; j < 16; j++) lds_get(lds[16 * w + j], lane, acc[j]);  // layout A
     if (16 * w < a.m) {  // d=4, group r = 16w
+      if constexpr (SHARED) {
+        fft4x4(acc, tf + 3 + w * 3);
+      } else {
 #pragma unroll
-      for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf + 3 + w * 3);
+        for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf + 3 + w * 3);
+      }
     }
 #pragma unroll
     for (int g = 0; g < 4; g++) {  // d=1, groups r = 16w + 4g
@@ -321,6 +376,20 @@ __device__ __forceinline__ void mac_sel(Sym<NV> &x, const Sel<NV> &s, const Tab 
   }
 }
 
+// One received input of the matrix kernels: orig[idx] or rec[idx]; with
+// kSrcXorScratch, rec[idx] ^ xs[idx] (a syndrome, reconstruct by syndromes).
+template <int NV>
+__device__ __forceinline__ void load_input(Sym<NV> &y, int32_t src, const uint8_t *orig, const uint8_t *rec,
+                                           const uint8_t *xs, uint64_t sb, uint32_t off, bool contig) {
+  const uint64_t o = static_cast<uint64_t>(src & kSrcIndexMask) * sb;
+  dev::load_sym(y, ((src & kSrcRecovery) ? rec : orig) + o, off, contig);
+  if (src & kSrcXorScratch) {
+    Sym<NV> z;
+    dev::load_sym(z, xs + o, off, contig);
+    dev::xor_into(y, z);
+  }
+}
+
 template <int E, int NV, int D>
 __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
   uint32_t off;
@@ -333,20 +402,18 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     const uint64_t s = blockIdx.y;
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
-    auto in_ptr = [&](uint32_t i) {
-      const int32_t src = srcs[i];
-      return ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb;
-    };
+    const uint8_t *xs = a.xsrc + s * a.xsrc_stripe_stride;
+    auto load_in = [&](Sym<NV> &y, uint32_t i) { load_input(y, srcs[i], orig, rec, xs, sb, off, a.contig); };
     Sym<NV> acc[E];
 #pragma unroll
     for (int j = 0; j < E; j++) dev::zero(acc[j]);
     if constexpr (D == 1) {
       // one input ahead: input i+1 in flight while input i is multiplied
       Sym<NV> y;
-      dev::load_sym(y, in_ptr(0), off, a.contig);
+      load_in(y, 0);
       for (uint32_t i = 0; i < n_in; i++) {
         Sym<NV> nxt = y;
-        if (i + 1 < n_in) dev::load_sym(nxt, in_ptr(i + 1), off, a.contig);
+        if (i + 1 < n_in) load_in(nxt, i + 1);
         Sel<NV> sel;
         make_sel(sel, y);
         const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
@@ -360,7 +427,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
         Sym<NV> y[D];
 #pragma unroll
         for (int d = 0; d < D; d++)
-          if (i0 + d < n_in) dev::load_sym(y[d], in_ptr(i0 + d), off, a.contig);
+          if (i0 + d < n_in) load_in(y[d], i0 + d);
 #pragma unroll
         for (int d = 0; d < D; d++) {
           if (i0 + d >= n_in) break;
@@ -397,19 +464,16 @@ __global__ __launch_bounds__(kBlock) void k_decode_mtile(DecodeArgs a) {
   const CI srcs = (CI)(a.pos_src);
   const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
   const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
-  auto in_ptr = [&](uint32_t i) {
-    const int32_t src = srcs[i];
-    return ((src & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(src & kSrcIndexMask) * sb;
-  };
+  const uint8_t *xs = a.xsrc + s * a.xsrc_stripe_stride;
   const uint32_t stride = 4 * EW;  // padded outputs per table row
   Sym<NV> acc[EW];
 #pragma unroll
   for (int j = 0; j < EW; j++) dev::zero(acc[j]);
   Sym<NV> y;
-  dev::load_sym(y, in_ptr(0), off, a.contig);
+  load_input(y, srcs[0], orig, rec, xs, sb, off, a.contig);
   for (uint32_t i = 0; i < a.n_in; i++) {
     Sym<NV> nxt = y;
-    if (i + 1 < a.n_in) dev::load_sym(nxt, in_ptr(i + 1), off, a.contig);
+    if (i + 1 < a.n_in) load_input(nxt, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
     Sel<NV> sel;
     make_sel(sel, y);
     const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * stride + j0;
@@ -563,7 +627,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
       const uint64_t t = j == 0 ? a.trunc_first : (j + 1 == a.n_chunks ? a.trunc_last : C);
       for (uint64_t p = 0; p < C; p++) {
         Sym<NV> v;
-        if (p < t) ld(v, src + (j * C + p) * sb);
+        if (p < t && !skipped(a, static_cast<uint32_t>(j * C + p))) ld(v, src + (j * C + p) * sb);
         else dev::zero(v);
         st(work + (j * C + p) * sb, v);
       }
@@ -968,6 +1032,7 @@ hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_
     b.orig += s0 * a.orig_stripe_stride;
     b.rec += s0 * a.rec_stripe_stride;
     b.out += s0 * a.out_stripe_stride;
+    if (b.xsrc) b.xsrc += s0 * a.xsrc_stripe_stride;
     b.tab_pre += s0 * a.pattern_stride;
     b.tab_post += s0 * a.pattern_stride;
     b.pos_src += s0 * a.pattern_stride;
@@ -994,8 +1059,15 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
     // one block per 64-lane region; 4 waves split the 64 positions
     const uint64_t regions = a.shard_bytes / 64 * (8 / kc.nv) / 64;
     const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
-    if (kc.nv == 1) hipLaunchKernelGGL(k_encode_ws64<1>, g, dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL(k_encode_ws64<2>, g, dim3(kBlock), 0, s, a);
+    const char *ev = getenv("RS_AMD_WS64_SHARED");  // A/B switch: 1 (default) shared stage tables
+    const bool shared = !(ev && ev[0] == '0');
+    if (kc.nv == 1) {
+      if (shared) hipLaunchKernelGGL((k_encode_ws64<1, true>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((k_encode_ws64<1, false>), g, dim3(kBlock), 0, s, a);
+    } else {
+      if (shared) hipLaunchKernelGGL((k_encode_ws64<2, true>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((k_encode_ws64<2, false>), g, dim3(kBlock), 0, s, a);
+    }
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_encode_generic<1>, grid, dim3(kBlock), 0, s, a);

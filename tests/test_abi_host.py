@@ -128,7 +128,15 @@ def test_kernel_selection(monkeypatch):
     monkeypatch.setenv("RS_AMD_JIT", "0")
     assert R.encode_kernel_name(10, 4, 1 << 20) == "encode_reg_w4_nv4"
     assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "decode_matrix_e4_nv4"
+    # wide code, 55 erasures: encode the received data, then the 55 x 55 syndrome solve
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+decode_mtile16_nv1"
+    present = [1] * 255
+    for i in (3, 77, 150, 199):
+        present[i] = 0
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18, present) == "decode_matrix_e4_nv4"  # 4 x 200 MACs cheaper
+    monkeypatch.setenv("RS_AMD_DECODE", "matrix")
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "decode_mtile16_nv1"
+    monkeypatch.delenv("RS_AMD_DECODE")
     assert R.reconstruct_kernel_name(200, 55, 320).startswith("decode_generic")
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"
     assert R.encode_kernel_name(100, 20, 1 << 18).startswith("encode_generic")
