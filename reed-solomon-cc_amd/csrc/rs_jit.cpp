@@ -173,12 +173,13 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //                        the compiler hoists the loads anyway)
 //   RS_AMD_NET_WAVES     amdgpu_waves_per_eu occupancy hint, 0 = none (default 0)
 //   RS_AMD_NET_NT        non-temporal loads/stores (default 1)
+//   RS_AMD_NET_UNITS     4 KiB units per wave, walked in a loop (default 1)
 //   RS_AMD_NET_BARRIER   sched_barrier between inputs: bounds the scheduling regions,
 //                        so compile time stays ~linear in size (1 on, 0 off, default
 //                        -1: on above 16 input blocks; off costs nothing to compile
 //                        for small networks and measured ~1.5% faster on RS(10,4))
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 1, barrier = -1;
+  int prefetch = 0, waves = 0, nt = 1, barrier = -1, units = 1;
 };
 
 int env_int(const char *name, int def) {
@@ -192,12 +193,13 @@ Tuning tuning() {
   t.waves = std::max(0, std::min(8, env_int("RS_AMD_NET_WAVES", t.waves)));
   t.nt = env_int("RS_AMD_NET_NT", t.nt) != 0;
   t.barrier = env_int("RS_AMD_NET_BARRIER", t.barrier);
+  t.units = std::max(1, std::min(64, env_int("RS_AMD_NET_UNITS", t.units)));
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
   return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt) + "b" +
-         std::to_string(t.barrier);
+         std::to_string(t.barrier) + "u" + std::to_string(t.units);
 }
 
 }  // namespace
@@ -221,14 +223,18 @@ std::string generate(const NetSpec &spec, const std::string &name) {
        "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0) {\n"
        "  const u32 lane = threadIdx.x & 63;\n"
     << "  const u32 tile = blockIdx.x % " << n_tiles << "u;\n"
-    << "  const u64 unit = (u64)(blockIdx.x / " << n_tiles << "u) * 4 + (threadIdx.x >> 6);\n"
-    << "  if (unit * 4096 >= sb) return;\n"
+    << "  const u64 ubase = ((u64)(blockIdx.x / " << n_tiles << "u) * 4 + (threadIdx.x >> 6)) * " << tu.units
+    << "u;\n"
        "  const u32 ll = lane & 31;\n"
-       "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n"
        "  const u64 s = stripe0 + blockIdx.y;\n"
        "  const unsigned char *B0 = b0 + s * s0;\n"
        "  const unsigned char *B1 = b1 + s * s1;\n"
-       "  unsigned char *O = out + s * so;\n";
+       "  unsigned char *O = out + s * so;\n"
+    << "#pragma unroll 1\n"
+    << "  for (u32 it = 0; it < " << tu.units << "u; it++) {\n"
+       "  const u64 unit = ubase + it;\n"
+       "  if (unit * 4096 >= sb) break;\n"
+       "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n";
   auto in_expr = [&](uint32_t t) {
     const int32_t src = spec.src[t];
     std::ostringstream e;
@@ -270,7 +276,7 @@ std::string generate(const NetSpec &spec, const std::string &name) {
     }
     o << "  }\n";
   }
-  o << "}\n";
+  o << "  }\n}\n";  // unit loop, kernel
   return o.str();
 }
 
@@ -373,6 +379,7 @@ const Kernel *get(const NetSpec &spec, std::string &err) {
   k->n_in = spec.n_in;
   k->n_out = spec.n_out;
   k->n_tiles = (spec.n_out + kTileOut - 1) / kTileOut;
+  k->units = static_cast<uint32_t>(tuning().units);
   k->name = name;
   k->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (std::getenv("RS_AMD_JIT_VERBOSE"))
@@ -386,7 +393,8 @@ const Kernel *get(const NetSpec &spec, std::string &err) {
 hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const uint8_t *buf1, uint64_t stride1,
                   uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s) {
   const uint64_t units = shard_bytes / kUnitBytes;
-  const uint32_t gx = static_cast<uint32_t>((units + 3) / 4 * k.n_tiles);
+  const uint64_t per_block = 4ull * k.units;
+  const uint32_t gx = static_cast<uint32_t>((units + per_block - 1) / per_block * k.n_tiles);
   for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
     const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
     const unsigned char *a0 = buf0, *a1 = buf1 ? buf1 : buf0;

@@ -50,7 +50,7 @@ std::string generate(const NetSpec &spec, const std::string &name);
 struct Kernel {
   hipModule_t module = nullptr;
   hipFunction_t fn = nullptr;
-  uint32_t n_in = 0, n_out = 0, n_tiles = 0;
+  uint32_t n_in = 0, n_out = 0, n_tiles = 0, units = 1;
   std::string name;
   double compile_ms = 0;
 };
