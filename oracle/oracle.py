@@ -54,6 +54,7 @@ def lib():
         L.rso_eval_poly.argtypes = [C.c_void_p, C.c_uint64]
         L.rso_use_high_rate.argtypes = [C.c_uint64, C.c_uint64]
         L.rso_encode.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, pp, pp, C.c_int]
+        L.rso_encode_low.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, pp, pp, C.c_int]
         L.rso_decode.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, pp, pp, pp, C.c_int]
         L.rso_encode_batch.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t, C.c_void_p,
                                        C.c_void_p, C.c_int, C.c_int]
@@ -145,6 +146,18 @@ def encode(k: int, m: int, original: np.ndarray, quirks: int = CORRECTED):
     ins = _ptr_array([original[i] for i in range(k)])
     outs = _ptr_array([rec[i] for i in range(m)])
     st = lib().rso_encode(k, m, sb, ins, outs, quirks)
+    return st, rec
+
+
+def encode_low(k: int, m: int, original: np.ndarray, quirks: int = CORRECTED):
+    """Low-rate encode (absent from the reference: PARITY UNPINNED, restated from
+    reed-solomon-simd's low-rate encoder). original [k, sb] -> (status, recovery [m, sb])."""
+    original = np.ascontiguousarray(original, dtype=np.uint8)
+    sb = original.shape[1]
+    rec = np.zeros((m, sb), np.uint8)
+    ins = _ptr_array([original[i] for i in range(k)])
+    outs = _ptr_array([rec[i] for i in range(m)])
+    st = lib().rso_encode_low(k, m, sb, ins, outs, quirks)
     return st, rec
 
 

@@ -539,6 +539,42 @@ int rso_encode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const 
   return RSO_OK;
 }
 
+/* Low-rate encode (useHighRate == false). ABSENT from the reference
+ * (root.zig:119-121 @panic("TODO")), so PARITY UNPINNED: restated from the
+ * algorithm the reference ports, reed-solomon-simd's low-rate encoder
+ * (benchmarks.zig:1-2 names the crate; it is not vendored here). Originals sit at
+ * positions [0, k) of one chunk C = ceilPow2(k): IFFT(pos 0, size C, trunc k,
+ * skew 0); recovery chunk j (shards [jC, jC + C)) = FFT of a copy of that chunk,
+ * trunc min(C, m - jC), skew (j + 1)C — i.e. evaluations at positions [C, C + m). */
+int rso_encode_low(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,
+                   uint8_t *const *recovery_out, int quirks) {
+  rso_init();
+  if (k == 0 || original == NULL) return RSO_ERR_TOO_FEW_ORIGINAL_SHARDS;
+  int hr = rso_use_high_rate(k, m);
+  if (hr < 0) return -hr;
+  if (hr == 1) return RSO_ERR_UNSUPPORTED_SHARD_COUNT; /* high rate: rso_encode */
+  if (shard_bytes == 0 || (shard_bytes & 1)) return RSO_ERR_INVALID_SHARD_SIZE;
+  size_t L = (shard_bytes + 63) / 64;
+  uint64_t C = ceil_pow2(k);
+  uint8_t *coef = calloc(C * L, 64), *tmp = malloc(C * L * 64);
+  if (!coef || !tmp) {
+    free(coef);
+    free(tmp);
+    return RSO_ERR_OUT_OF_MEMORY;
+  }
+  for (uint64_t i = 0; i < k; i++) insert_shard(SHARD(coef, L, i), original[i], shard_bytes);
+  rso_ifft(coef, L, 0, C, k, 0, quirks);
+  for (uint64_t cs = 0; cs < m; cs += C) {
+    uint64_t t = m - cs < C ? m - cs : C;
+    memcpy(tmp, coef, C * L * 64);
+    rso_fft(tmp, L, 0, C, t, cs + C, quirks);
+    for (uint64_t i = 0; i < t; i++) extract_shard(recovery_out[cs + i], SHARD(tmp, L, i), shard_bytes);
+  }
+  free(coef);
+  free(tmp);
+  return RSO_OK;
+}
+
 /* Decoder.decode on a prepared work buffer (root.zig:268-335).
  * work: [Wdec][L][64]; received[pos] marks present positions (recovery at
  * [0,m), originals at [chunk, chunk+k)). Restored originals land in place. */

@@ -86,6 +86,9 @@ int rso_use_high_rate(uint64_t k, uint64_t m);
  * shard_bytes % 64 bytes uses the last-chunk layout root.zig:338-348 implies) */
 int rso_encode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,
                uint8_t *const *recovery_out, int quirks);
+/* low-rate encode (absent from the reference, parity unpinned; see rs_oracle.c) */
+int rso_encode_low(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,
+                   uint8_t *const *recovery_out, int quirks);
 /* original[i] / recovery[i] == NULL marks a missing shard; restored_out has k
  * slots and receives every original (copied for present ones). */
 int rso_decode(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *const *original,

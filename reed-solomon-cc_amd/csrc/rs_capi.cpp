@@ -76,11 +76,16 @@ int use_high_rate(uint64_t original, uint64_t recovery) {
   return original <= recovery ? 1 : 0;
 }
 
+constexpr uint64_t kLowRateMaxRecovery = 64;
+inline bool recovery_ok_low_rate(uint64_t m) { return m <= kLowRateMaxRecovery; }
+
 // Encoder.init / Decoder.init checks (root.zig:100-103, 198-201) + the tail panic (root.zig:385)
 int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
   const int hr = use_high_rate(k, m);
   if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
-  if (hr == 0) return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec (reference panics, root.zig:120)");
+  // low rate: the reference panics (root.zig:120); here up to 64 recovery shards (§8 f4)
+  if (hr == 0 && recovery_ok_low_rate(m) == false)
+    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec with more than 64 recovery shards");
   if (shard_bytes == 0 || (shard_bytes & 1)) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes is 0 or odd");
   // shard_bytes % 64 != 0: the reference panics (root.zig:385); handled here with
   // the tail layout of root.zig:338-348 (tail_* below).
@@ -532,6 +537,201 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
 
 constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
 
+// ------------------------------------------------------- low-rate codec (§8 f4)
+// The reference panics on low rate (root.zig:119-121, 226-228). Here the encode
+// is reed-solomon-simd's low-rate encoder (rs_gf.hpp scalar_encode_low; parity
+// unpinned: no reference output exists) and a reconstruct is the unique MDS
+// solution, derived by linear algebra from the encode map. Both run as maps on
+// the network kernels, or on the table matrix kernels in groups of <= 8 outputs.
+bool is_low_rate(uint64_t k, uint64_t m) { return use_high_rate(k, m) == 0; }
+
+void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
+  const bool d1 = flags & RS_FLAG_QUIRK_D1;
+  ns.role = "encode_low";
+  ns.n_in = static_cast<uint32_t>(k);
+  ns.n_out = static_cast<uint32_t>(m);
+  ns.src.clear();
+  ns.images.assign(k * m * 16, 0);
+  std::vector<uint16_t> in(k, 0), out(m);
+  for (uint64_t t = 0; t < k; t++) {
+    ns.src.push_back(static_cast<int32_t>(t));
+    for (int b = 0; b < 16; b++) {
+      in[t] = static_cast<uint16_t>(1u << b);
+      scalar_encode_low(in.data(), k, m, d1, out.data());
+      for (uint64_t j = 0; j < m; j++) ns.images[(t * m + j) * 16 + b] = out[j];
+    }
+    in[t] = 0;
+  }
+}
+
+// Reconstruct of a systematic linear code with encode map G (G.images[(t*m + r)*16 + b]
+// = parity r of basis b at data t): with E the erased data, P the present data and R
+// the first e present recovery rows, p_R = G_RE x + G_RP d_P, so
+// x = G_RE^-1 (p_R + G_RP d_P): a map from [d_P, p_R] to x (16e x 16e GF(2) solve).
+int linear_decode_map(uint64_t k, uint64_t m, const jit::NetSpec &G, const uint8_t *present, const char *role,
+                      jit::NetSpec &ns) {
+  std::vector<uint64_t> E, P, Rr;
+  for (uint64_t i = 0; i < k; i++) (present[i] ? P : E).push_back(i);
+  for (uint64_t r = 0; r < m && Rr.size() < E.size(); r++)
+    if (present[k + r]) Rr.push_back(r);
+  const size_t e = E.size(), np = P.size();
+  if (Rr.size() < e) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+  const size_t N = 16 * e, cols = N + 16 * np + N, words = (cols + 63) / 64;
+  auto g = [&](uint64_t t, uint64_t r, int b) { return G.images[(t * m + r) * 16 + b]; };
+  std::vector<std::vector<uint64_t>> M(N, std::vector<uint64_t>(words, 0));
+  auto set = [&](size_t row, size_t col) { M[row][col / 64] |= 1ull << (col % 64); };
+  for (size_t j = 0; j < e; j++)
+    for (int c = 0; c < 16; c++) {
+      const size_t row = 16 * j + c;
+      for (size_t t = 0; t < e; t++)  // [G_RE | G_RP | I]
+        for (int b = 0; b < 16; b++)
+          if (g(E[t], Rr[j], b) >> c & 1) set(row, 16 * t + b);
+      for (size_t t = 0; t < np; t++)
+        for (int b = 0; b < 16; b++)
+          if (g(P[t], Rr[j], b) >> c & 1) set(row, N + 16 * t + b);
+      set(row, N + 16 * np + row);
+    }
+  for (size_t col = 0; col < N; col++) {  // Gauss-Jordan over GF(2)
+    size_t piv = col;
+    while (piv < N && !(M[piv][col / 64] >> (col % 64) & 1)) piv++;
+    if (piv == N) return fail(RS_ERR_DEVICE, "decode matrix singular");
+    std::swap(M[piv], M[col]);
+    for (size_t r = 0; r < N; r++)
+      if (r != col && (M[r][col / 64] >> (col % 64) & 1))
+        for (size_t w = 0; w < words; w++) M[r][w] ^= M[col][w];
+  }
+  // x = [G_RE^-1 G_RP | G_RE^-1] [d_P; p_R]
+  ns.role = role;
+  ns.n_in = static_cast<uint32_t>(np + e);
+  ns.n_out = static_cast<uint32_t>(e);
+  ns.src.clear();
+  for (uint64_t i : P) ns.src.push_back(static_cast<int32_t>(i));
+  for (uint64_t r : Rr) ns.src.push_back(kSrcRecovery | static_cast<int32_t>(r));
+  ns.images.assign(static_cast<size_t>(ns.n_in) * e * 16, 0);
+  for (size_t i = 0; i < ns.n_in; i++)
+    for (int b = 0; b < 16; b++) {
+      const size_t col = N + 16 * i + b;
+      for (size_t j = 0; j < e; j++)
+        for (int c = 0; c < 16; c++)
+          if (M[16 * j + c][col / 64] >> (col % 64) & 1) ns.images[(i * e + j) * 16 + b] |= static_cast<uint16_t>(1u << c);
+    }
+  return RS_OK;
+}
+
+// A map on the device: the network kernel when it fits, else the table matrix
+// kernels over groups of <= 8 outputs (blocks [group][n_in][E_g] of tables + src).
+struct MapPlan {
+  std::shared_ptr<DevBuf> buf;
+  uint32_t n_in = 0, n_out = 0;
+  std::vector<size_t> group_off;  // byte offset of each group's table block
+  size_t off_src = 0;
+  std::shared_ptr<NetSlot> net;
+};
+std::map<std::string, std::shared_ptr<MapPlan>> g_map_plans;
+
+int build_map_plan(int dev, jit::NetSpec &&spec, std::shared_ptr<MapPlan> &out) {
+  auto p = std::make_shared<MapPlan>();
+  p->n_in = spec.n_in;
+  p->n_out = spec.n_out;
+  std::vector<RsTab> tabs;
+  for (uint32_t j0 = 0; j0 < spec.n_out; j0 += kMatrixMaxOut) {
+    const uint32_t eg = std::min<uint32_t>(kMatrixMaxOut, spec.n_out - j0);
+    p->group_off.push_back(tabs.size() * sizeof(RsTab));
+    for (uint32_t t = 0; t < spec.n_in; t++)
+      for (uint32_t j = 0; j < eg; j++)
+        tabs.push_back(make_tab_from_images(&spec.images[(static_cast<size_t>(t) * spec.n_out + j0 + j) * 16]));
+  }
+  std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + spec.n_in * sizeof(int32_t));
+  std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
+  std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), spec.src.data(), spec.n_in * sizeof(int32_t));
+  p->off_src = tabs.size() * sizeof(RsTab);
+  int st = upload(blob.data(), blob.size(), dev, p->buf);
+  if (st) return st;
+  p->net = std::make_shared<NetSlot>();
+  p->net->spec = std::move(spec);
+  out = p;
+  return RS_OK;
+}
+
+// out[j] = sum_i map_ij(in_i) for every stripe; inputs per src (buffer 0 / 1).
+int run_map(const MapPlan &p, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0, const uint8_t *b1, uint64_t s1,
+            uint8_t *out, uint64_t so, int max_nv, hipStream_t s) {
+  if (!b0) b0 = b1;
+  if (!b1) b1 = b0;
+  if (max_nv == 4 && jit::enabled() && jit::supports(p.n_in, p.n_out, sb))
+    if (const jit::Kernel *nk = net_kernel(*p.net)) {
+      HIP_TRY(jit::launch(*nk, b0, s0, b1, s1, out, so, sb, n, s));
+      return RS_OK;
+    }
+  const uint8_t *base = static_cast<const uint8_t *>(p.buf->p);
+  for (size_t g = 0; g < p.group_off.size(); g++) {
+    const uint32_t j0 = static_cast<uint32_t>(g * kMatrixMaxOut);
+    const uint32_t eg = std::min<uint32_t>(kMatrixMaxOut, p.n_out - j0);
+    const KernelChoice kc = choose_decode_matrix(eg, sb, max_nv);
+    DecodeArgs a{};
+    a.orig = b0;
+    a.orig_stripe_stride = s0;
+    a.rec = b1;
+    a.rec_stripe_stride = s1;
+    a.out = out + static_cast<uint64_t>(j0) * sb;
+    a.out_stripe_stride = so;
+    a.shard_bytes = sb;
+    a.tab_mat = reinterpret_cast<const RsTab *>(base + p.group_off[g]);
+    a.pos_src = reinterpret_cast<const int32_t *>(base + p.off_src);
+    a.n_in = p.n_in;
+    a.n_out = eg;
+    a.contig = contig_ok(sb, kc.nv);
+    a.n_stripes = n;
+    // launch_decode advances these per 65535-stripe slice: keep them valid
+    a.tab_pre = a.tab_post = a.tab_mat;
+    a.pos_dst = a.pos_src;
+    HIP_TRY(launch_decode(kc, a, s));
+  }
+  return RS_OK;
+}
+
+int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<MapPlan> &out) {
+  const std::string key = "lowenc/" + std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                          std::to_string(flags & RS_FLAG_QUIRK_D1);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_map_plans.find(key);
+  if (it != g_map_plans.end()) {
+    out = it->second;
+    return RS_OK;
+  }
+  jit::NetSpec spec;
+  encode_low_map(k, m, flags, spec);
+  int st = build_map_plan(dev, std::move(spec), out);
+  if (st) return st;
+  g_map_plans.emplace(key, out);
+  return RS_OK;
+}
+
+int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns) {
+  jit::NetSpec G;
+  encode_low_map(k, m, flags, G);
+  return linear_decode_map(k, m, G, present, "reconstruct_low", ns);
+}
+
+int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present,
+                        std::shared_ptr<MapPlan> &out) {
+  std::string key = "lowdec/" + std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                    std::to_string(flags & RS_FLAG_QUIRK_D1) + "/";
+  for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto it = g_map_plans.find(key);
+  if (it != g_map_plans.end()) {
+    out = it->second;
+    return RS_OK;
+  }
+  jit::NetSpec spec;
+  int st = low_decode_map(k, m, flags, present, spec);
+  if (st) return st;
+  if ((st = build_map_plan(dev, std::move(spec), out))) return st;
+  g_map_plans.emplace(key, out);
+  return RS_OK;
+}
+
 // ---------------------------------------------------------- shard tails
 // Batches whose shard_bytes is not a multiple of 64 run on padded copies
 // ([stripe][shard][ceil(sb/64)*64], tail chunk in the reference's layout) in
@@ -655,6 +855,11 @@ static const char *net_name(const char *role, uint64_t n_in, uint64_t n_out) {
 }
 
 const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
+  if (is_low_rate(k, m)) {
+    if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))
+      return net_name("encode_low", k, m);
+    return "lowrate_matrix";
+  }
   if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name("encode", k, m);
   return choose_encode(k, m, sb, 4).name;
 }
@@ -668,6 +873,11 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   uint64_t e = 0, have = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
+  if (is_low_rate(k, m)) {
+    if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
+      return net_name("reconstruct_low", k, e);
+    return "lowrate_matrix";
+  }
   const std::string mode = decode_mode_env();
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
@@ -694,7 +904,13 @@ int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_
     uint64_t have = 0;
     for (uint64_t i = 0; i < k + m; i++) have += present[i] != 0;
     if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
-    reconstruct_map(k, m, flags, present, spec);
+    if (is_low_rate(k, m)) {
+      if ((st = low_decode_map(k, m, flags, present, spec))) return st;
+    } else {
+      reconstruct_map(k, m, flags, present, spec);
+    }
+  } else if (is_low_rate(k, m)) {
+    encode_low_map(k, m, flags, spec);
   } else {
     encode_map(k, m, flags, spec);
   }
@@ -726,9 +942,15 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
   if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
   int dev;
   if ((st = current_device(&dev))) return st;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (is_low_rate(k, m)) {
+    std::shared_ptr<MapPlan> lp;
+    if ((st = get_low_encode_plan(dev, k, m, flags, lp))) return st;
+    return run_map(*lp, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
+                   static_cast<uint8_t *>(d_recovery), rec_stride, max_nv, s);
+  }
   std::shared_ptr<EncodePlan> plan;
   if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
-  hipStream_t s = static_cast<hipStream_t>(stream);
   if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
     if (const jit::Kernel *nk = net_kernel(*plan->net)) {
@@ -812,6 +1034,13 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
   int dev;
   if ((st = current_device(&dev))) return st;
+  if (is_low_rate(k, m)) {
+    std::shared_ptr<MapPlan> lp;
+    if ((st = get_low_decode_plan(dev, k, m, flags, present, lp))) return st;
+    return run_map(*lp, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride,
+                   static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored), out_stride,
+                   max_nv, static_cast<hipStream_t>(stream));
+  }
   std::shared_ptr<DecodePlan> plan;
   if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
   if (plan->net && max_nv == 4) {
@@ -985,6 +1214,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
                                       void *d_restored, uint64_t out_stride, int32_t *d_status, uint32_t flags,
                                       rs_stream_t stream) {
   int st = check_codec(k, m, sb);
+  if (st == RS_OK && is_low_rate(k, m))
+    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "per-stripe patterns: high-rate codes only");
   if (st) return st;
   if (n_stripes == 0 || max_e == 0) return RS_OK;
   if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");

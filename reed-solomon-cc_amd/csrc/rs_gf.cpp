@@ -224,6 +224,19 @@ void scalar_encode(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, bo
   for (uint64_t i = 0; i < m; i++) out[i] = acc[i];
 }
 
+void scalar_encode_low(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, uint16_t *out) {
+  const uint64_t C = ceil_pow2(k);
+  std::vector<uint16_t> coef(C, 0), tmp(C);
+  for (uint64_t i = 0; i < k; i++) coef[i] = in[i];
+  scalar_ifft(coef.data(), C, k, 0, quirk_d1);  // originals at positions [0, k)
+  for (uint64_t cs = 0; cs < m; cs += C) {       // recovery chunk at positions [C + cs, ...)
+    tmp = coef;
+    const uint64_t t = std::min(C, m - cs);
+    scalar_fft(tmp.data(), C, t, cs + C, quirk_d1);
+    for (uint64_t i = 0; i < t; i++) out[cs + i] = tmp[i];
+  }
+}
+
 RsTab make_twiddle(uint32_t skew_index, bool quirk_d1) {
   if (skew_index >= kModulus) {  // beyond the table: only reachable for groups the device skips
     RsTab z{};

@@ -76,6 +76,13 @@ void scalar_reconstruct(uint16_t *sym, const uint8_t *received, const uint16_t *
 // Encoder.encode (root.zig:136-173) on one symbol per shard: in[k] -> out[m]
 // (used to derive the encode map for the bit-sliced network kernels).
 void scalar_encode(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, bool quirk_d2, uint16_t *out);
+// Low-rate encode (pow2(k) < pow2(m), or equal with k > m), on one symbol per shard.
+// The reference has none (root.zig:119-121 @panic("TODO")); restated from the
+// algorithm it ports, reed-solomon-simd's low-rate encoder (named in
+// benchmarks.zig:1-2, not vendored: parity unpinned): originals at positions
+// [0, k) of a chunk C = ceilPow2(k): IFFT(size C, trunc k, skew 0); recovery
+// chunk j = FFT(copy, size C, trunc min(C, m - jC), skew (j+1)C).
+void scalar_encode_low(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, uint16_t *out);
 // IFFT chunk truncations of the encode schedule (root.zig:143-166; D2 drops the last full chunk)
 std::vector<uint64_t> encode_chunk_truncs(uint64_t k, uint64_t m, bool quirk_d2);
 // root.zig:277-289: erasure flags for a received pattern -> evalPoly -> logs (65536 entries)

@@ -36,7 +36,7 @@ struct NetSpec {
 // must be a multiple of this, and below 4 GiB (32-bit lane offsets).
 constexpr uint64_t kUnitBytes = 4096;
 constexpr uint32_t kTileOut = 4;      // outputs per wave (64 accumulator planes)
-constexpr uint32_t kMaxOut = 16;      // tiles of kTileOut, one workgroup each
+constexpr uint32_t kMaxOut = 64;      // tiles of kTileOut, one workgroup each
 // generated code size: n_in x tiles input blocks of ~270 instructions each; hipRTC
 // takes ~20-40 ms per block, so the cap keeps a plan's compile near 1-2 s
 constexpr uint64_t kMaxBlocks = 64;

@@ -1,0 +1,137 @@
+"""Low-rate codec: pow2(k) < pow2(m), or equal with k > m.
+
+The reference panics here (root.zig:119-121, 226-228), so there is no reference
+output to pin: PARITY UNPINNED. The encode follows reed-solomon-simd's low-rate
+encoder (the crate the reference ports, benchmarks.zig:1-2), restated in the
+oracle (rso_encode_low) and in the library (rs_gf.cpp scalar_encode_low); the
+GPU encode is checked against that restatement, and reconstruct — unique for an
+MDS code — by round trips. The CPU tests pin the restatement's MDS property:
+every k-subset of a codeword determines the data (GF(2) rank of the 16k x 16k
+generator block)."""
+import itertools
+
+import numpy as np
+import pytest
+
+from rs_amd import reedsol_amd as R
+
+LOW_KM = [(1, 2), (2, 4), (3, 5), (3, 6), (5, 9), (4, 16), (10, 20), (7, 40), (16, 64)]
+
+
+def gf2_rank(rows):
+    rows = [int(r) for r in rows]
+    rank = 0
+    for bit in range(max((r.bit_length() for r in rows), default=0) - 1, -1, -1):
+        piv = next((i for i in range(rank, len(rows)) if rows[i] >> bit & 1), None)
+        if piv is None:
+            continue
+        rows[rank], rows[piv] = rows[piv], rows[rank]
+        for i in range(len(rows)):
+            if i != rank and rows[i] >> bit & 1:
+                rows[i] ^= rows[rank]
+        rank += 1
+    return rank
+
+
+def generator_columns(oracle, k, m):
+    """cols[s][b] = bit vector (16 (k+m) bits) of the codeword of basis symbol b at data shard s."""
+    cols = []
+    for s in range(k):
+        for b in range(16):
+            data = np.zeros((k, 64), np.uint8)
+            data[s, 0] = (1 << b) & 0xFF  # symbol 0: lo byte at [0], hi byte at [32]
+            data[s, 32] = (1 << b) >> 8
+            st, rec = oracle.encode_low(k, m, data)
+            assert st == 0
+            word = [int(data[i, 0]) | int(data[i, 32]) << 8 for i in range(k)]
+            word += [int(rec[r, 0]) | int(rec[r, 32]) << 8 for r in range(m)]
+            cols.append(word)
+    return cols
+
+
+@pytest.mark.parametrize("k,m", [(1, 2), (2, 4), (3, 5), (3, 6), (4, 7)])
+def test_low_rate_restatement_is_mds(oracle, k, m):
+    assert R.use_high_rate(k, m) is False
+    cols = generator_columns(oracle, k, m)
+    for keep in itertools.combinations(range(k + m), k):
+        # rows of the 16k x 16k block: for each basis input, its symbols on the kept shards
+        rows = []
+        for word in cols:
+            v = 0
+            for idx, sh in enumerate(keep):
+                v |= word[sh] << (16 * idx)
+            rows.append(v)
+        assert gf2_rank(rows) == 16 * k, keep
+
+
+@pytest.mark.parametrize("k,m", LOW_KM)
+def test_low_rate_network_compiles(k, m):
+    if k * ((m + 3) // 4) > 64:  # beyond the network size cap: table kernels only
+        pytest.skip("no network form")
+    assert R.net_compile_check(k, m) > 0
+
+
+def test_low_rate_limits():
+    with pytest.raises(R.LowRateUnsupported):
+        R.Encoder(2, 100, 64)
+    assert R.encode_kernel_name(10, 20, 1 << 16) == "net_encode_low_i10_o20"
+    assert R.encode_kernel_name(16, 64, 1 << 16) == "lowrate_matrix"
+
+
+# ----------------------------------------------------------------- GPU
+torch = pytest.importorskip("torch")
+gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("k,m", LOW_KM)
+@pytest.mark.parametrize("jit", ["1", "0"])
+@pytest.mark.parametrize("sb", [192, 8192])
+def test_low_rate_gpu_vs_oracle_and_roundtrip(oracle, monkeypatch, k, m, jit, sb):
+    monkeypatch.setenv("RS_AMD_JIT", jit)
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(k * 97 + m + sb)
+    n = 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
+    d = torch.from_numpy(data).to(dev)
+    R.encode_batch_dev(k, m, d, par)
+    torch.cuda.synchronize()
+    got = par.cpu().numpy()
+    for s in range(n):
+        st, exp = oracle.encode_low(k, m, data[s])
+        assert st == 0
+        assert (got[s] == exp).all(), (k, m, s)
+    for trial in range(3):
+        e = int(rng.integers(1, k + 1))
+        lost = list(rng.choice(k, size=e, replace=False))
+        extra = int(rng.integers(0, m - e + 1))
+        lost += [k + int(i) for i in rng.choice(m, size=extra, replace=False)]
+        present = np.ones(k + m, np.uint8)
+        present[lost] = 0
+        missing = [i for i in range(k) if not present[i]]
+        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8, device=dev)
+        R.reconstruct_batch_dev(k, m, present, d, par, out)
+        torch.cuda.synchronize()
+        assert (out.cpu().numpy() == data[:, missing]).all(), (k, m, sorted(lost))
+
+
+@pytest.mark.gpu
+@gpu
+def test_low_rate_exhaustive_rs3_5_one_shot():
+    """tests.zig:61-102's protocol on a low-rate code: every presence mask of RS(3,5)."""
+    k, m = 3, 5
+    orig = [bytes((i * 7 + j) % 256 for j in range(64)) for i in range(k)]
+    rec = R.encode(k, m, orig)
+    ok = 0
+    for mask in range(1 << (k + m)):
+        o = [None if mask >> i & 1 else orig[i] for i in range(k)]
+        r = [None if mask >> (k + i) & 1 else rec[i] for i in range(m)]
+        if bin(mask).count("1") <= m:
+            assert R.decode(k, m, o, r) == orig, mask
+            ok += 1
+        else:
+            with pytest.raises(R.NotEnoughShards):
+                R.decode(k, m, o, r)
+    assert ok == sum(1 for mask in range(1 << 8) if bin(mask).count("1") <= 5)
