@@ -48,11 +48,14 @@ __device__ __forceinline__ void tr8(u32 *x) {
   TRS(0, 2, 0x33333333u) TRS(1, 2, 0x33333333u) TRS(4, 2, 0x33333333u) TRS(5, 2, 0x33333333u)
   TRS(0, 1, 0x55555555u) TRS(2, 1, 0x55555555u) TRS(4, 1, 0x55555555u) TRS(6, 1, 0x55555555u)
 }
-#if RS_NT
+#if RS_NT & 1
 #define LDV(p) __builtin_nontemporal_load((const v4 *)(p))
-#define STV(v, p) __builtin_nontemporal_store((v), (v4 *)(p))
 #else
 #define LDV(p) (*(const v4 *)(p))
+#endif
+#if RS_NT & 2
+#define STV(v, p) __builtin_nontemporal_store((v), (v4 *)(p))
+#else
 #define STV(v, p) (*(v4 *)(p) = (v))
 #endif
 struct Raw { v4 a0, a1, b0, b1; };
@@ -172,14 +175,14 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //   RS_AMD_NET_PREFETCH  inputs loaded ahead of the one being transformed (default 0;
 //                        the compiler hoists the loads anyway)
 //   RS_AMD_NET_WAVES     amdgpu_waves_per_eu occupancy hint, 0 = none (default 0)
-//   RS_AMD_NET_NT        non-temporal loads/stores (default 1)
+//   RS_AMD_NET_NT        non-temporal loads (bit 0) / stores (bit 1), default 3
 //   RS_AMD_NET_UNITS     4 KiB units per wave, walked in a loop (default 1)
 //   RS_AMD_NET_BARRIER   sched_barrier between inputs: bounds the scheduling regions,
 //                        so compile time stays ~linear in size (1 on, 0 off, default
 //                        -1: on above 16 input blocks; off costs nothing to compile
 //                        for small networks and measured ~1.5% faster on RS(10,4))
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 1, barrier = -1, units = 1;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1;
 };
 
 int env_int(const char *name, int def) {
@@ -191,7 +194,7 @@ Tuning tuning() {
   Tuning t;
   t.prefetch = std::max(0, std::min(8, env_int("RS_AMD_NET_PREFETCH", t.prefetch)));
   t.waves = std::max(0, std::min(8, env_int("RS_AMD_NET_WAVES", t.waves)));
-  t.nt = env_int("RS_AMD_NET_NT", t.nt) != 0;
+  t.nt = env_int("RS_AMD_NET_NT", t.nt) & 3;
   t.barrier = env_int("RS_AMD_NET_BARRIER", t.barrier);
   t.units = std::max(1, std::min(64, env_int("RS_AMD_NET_UNITS", t.units)));
   return t;

@@ -488,6 +488,84 @@ __global__ __launch_bounds__(kBlock) void k_decode_mtile(DecodeArgs a) {
     if (j0 + j < a.n_out) dev::store_sym(out + static_cast<uint64_t>(j0 + j) * sb, off, acc[j], a.contig);
 }
 
+// Same product with VGPR tables: every v_perm_b32 then has only VGPR operands,
+// where SGPR tables cost one SGPR->VGPR v_mov per table pair (gfx9 VOP3 reads at
+// most one SGPR) — ~0.74 moves per v_perm in k_decode_mtile's ISA.
+template <int NV>
+__device__ __forceinline__ void mac_sel_v(Sym<NV> &x, const Sel<NV> &s, const uint32_t *lo, const uint32_t *hi) {
+  using dev::perm;
+  using dev::xor3;
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    uint32_t l = xor3(x.l[v], perm(lo[1], lo[0], s.a0[v]), perm(lo[3], lo[2], s.a1[v]));
+    uint32_t h = xor3(x.h[v], perm(hi[1], hi[0], s.a0[v]), perm(hi[3], hi[2], s.a1[v]));
+    l = xor3(l, perm(lo[4], lo[4], s.a2[v]), perm(lo[6], lo[5], s.b0[v]));
+    h = xor3(h, perm(hi[4], hi[4], s.a2[v]), perm(hi[6], hi[5], s.b0[v]));
+    x.l[v] = xor3(l, perm(lo[8], lo[7], s.b1[v]), perm(lo[9], lo[9], s.b2[v]));
+    x.h[v] = xor3(h, perm(hi[8], hi[7], s.b1[v]), perm(hi[9], hi[9], s.b2[v]));
+  }
+}
+
+// k_decode_mtile with the tables of each input row staged in LDS (double-buffered,
+// one barrier per input) and read back as VGPRs by broadcast ds_read_b128; waves
+// past n_out still stage and join the barriers, and padded outputs are skipped.
+template <int EW, int NV>
+__global__ __launch_bounds__(kBlock) void k_decode_mtile_lds(DecodeArgs a) {
+  constexpr int kRow = 4 * EW;  // outputs per table row (4 waves)
+  __shared__ uint4 tabs[2][kRow][5];  // lo[10] hi[10] of each RsTab
+  const uint64_t sb = a.shard_bytes;
+  if (blockIdx.x >= sb / 64 * (8 / NV) / 64) return;  // uniform over the block
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t j0 = w * EW;
+  const uint32_t nj = j0 < a.n_out ? min(static_cast<uint32_t>(EW), a.n_out - j0) : 0u;
+  const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
+  const uint64_t s = blockIdx.y;
+  typedef const __attribute__((address_space(4))) int32_t *CI;
+  const CI srcs = (CI)(a.pos_src);
+  const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
+  const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
+  const uint8_t *xs = a.xsrc + s * a.xsrc_stripe_stride;
+  auto stage = [&](uint32_t i, int b) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.tab_mat + static_cast<uint64_t>(i) * kRow);
+    for (uint32_t q = threadIdx.x; q < kRow * 5; q += kBlock) tabs[b][q / 5][q % 5] = src[q / 5 * 6 + q % 5];
+  };
+  Sym<NV> acc[EW];
+#pragma unroll
+  for (int j = 0; j < EW; j++) dev::zero(acc[j]);
+  stage(0, 0);
+  __syncthreads();
+  Sym<NV> y;
+  if (nj) load_input(y, srcs[0], orig, rec, xs, sb, off, a.contig);
+  for (uint32_t i = 0; i < a.n_in; i++) {
+    Sym<NV> nxt = y;
+    if (i + 1 < a.n_in) {
+      stage(i + 1, (i + 1) & 1);
+      if (nj) load_input(nxt, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
+    }
+    if (nj) {
+      Sel<NV> sel;
+      make_sel(sel, y);
+#pragma unroll
+      for (int j = 0; j < EW; j++) {
+        if (static_cast<uint32_t>(j) < nj) {  // uniform; keeps acc[] in registers (no dynamic index)
+          const uint4 *t = tabs[i & 1][j0 + j];
+          const uint4 q0 = t[0], q1 = t[1], q2 = t[2], q3 = t[3], q4 = t[4];
+          const uint32_t lo[10] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y};
+          const uint32_t hi[10] = {q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w};
+          mac_sel_v(acc[j], sel, lo, hi);
+        }
+      }
+    }
+    __syncthreads();  // buffer (i & 1) free for input i + 2
+    y = nxt;
+  }
+  uint8_t *out = a.out + s * a.out_stripe_stride;
+#pragma unroll
+  for (int j = 0; j < EW; j++)
+    if (static_cast<uint32_t>(j) < nj) dev::store_sym(out + static_cast<uint64_t>(j0 + j) * sb, off, acc[j], a.contig);
+}
+
 // ============================================ generic: column walk in HBM scratch
 template <int NV>
 __device__ __forceinline__ void ld(Sym<NV> &s, const uint8_t *p) {
@@ -1088,8 +1166,15 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
   if (kc.variant == Variant::kMatrixTiled) {
     const uint64_t regions = a.shard_bytes / 64 * (8 / kc.nv) / 64;
     const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
-    if (kc.nv == 1) hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
-    else hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
+    const char *ev = getenv("RS_AMD_MTILE_LDS");  // A/B switch: 1 (default) LDS-staged VGPR tables
+    if (!(ev && ev[0] == '0')) {
+      if (kc.nv == 1) hipLaunchKernelGGL((k_decode_mtile_lds<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((k_decode_mtile_lds<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
+    } else if (kc.nv == 1) {
+      hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
+    }
     return hipGetLastError();
   }
   if (kc.variant == Variant::kMatrix) {
