@@ -90,8 +90,17 @@ def cpu_baseline(k, m, sb, erase, budget_s):
                           "sample_stripes": s1},
         "encode_GiBps": round(gib * st / et, 3),
         "reconstruct_GiBps": round(gib * st / rt, 3),
+        "harness": harness_protocol(O),
         "cpu_model": _cpu_model(),
     }
+
+
+def harness_protocol(O, iters=2000):
+    """The reference's own benchmark (benchmarks.zig:11-60): mean microseconds per
+    single-threaded insert + encode of (32,32) and (64,64) at 1 KiB shards, random
+    bytes, timed natively in the oracle (rso_bench_encode, AVX2 engine)."""
+    return {f"encode:{k}/{m} 1KiB us": round(O.bench_encode_ns(k, m, 1024, iters) / 1e3, 3)
+            for k, m in ((32, 32), (64, 64))}
 
 
 def _cpu_model():

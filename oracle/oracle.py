@@ -61,6 +61,8 @@ def lib():
         L.rso_reconstruct_batch.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, C.c_size_t, C.c_void_p,
                                             C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.rso_force_scalar.argtypes = [C.c_int]
+        L.rso_bench_encode.restype = C.c_double
+        L.rso_bench_encode.argtypes = [C.c_uint64, C.c_uint64, C.c_size_t, C.c_uint64, C.c_int]
         L.rso_init()
         _lib = L
     return _lib
@@ -198,3 +200,8 @@ def reconstruct_batch(k, m, present: np.ndarray, shards: np.ndarray, quirks=CORR
 
 def force_scalar(on: bool):
     lib().rso_force_scalar(1 if on else 0)
+
+
+def bench_encode_ns(k, m, shard_bytes, iters, quirks=CORRECTED) -> float:
+    """benchmarks.zig:14-61 protocol timed natively: mean ns per insert + encode."""
+    return lib().rso_bench_encode(k, m, shard_bytes, iters, quirks)

@@ -19,6 +19,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #if defined(__x86_64__)
 #include <immintrin.h>
@@ -777,4 +778,39 @@ int rso_reconstruct_batch(uint64_t k, uint64_t m, size_t shard_bytes, size_t n_s
   p.present = present;
   p.quirks = quirks;
   return run_batch(p, n_stripes, threads);
+}
+
+/* benchmarks.zig:14-61 protocol, natively: mean ns per encode of k originals of
+ * shard_bytes random bytes (insert + encode timed; the work buffer is allocated
+ * outside the timed region, like the reference's untimed Encoder.init). */
+double rso_bench_encode(uint64_t k, uint64_t m, size_t shard_bytes, uint64_t iters, int quirks) {
+  rso_init();
+  if (check_codec(k, m, shard_bytes)) return -1.0;
+  size_t L = (shard_bytes + 63) / 64;
+  uint64_t chunk = ceil_pow2(m);
+  uint64_t work_count = (k + chunk - 1) / chunk * chunk;
+  uint8_t *orig = malloc(k * shard_bytes), *work = calloc(work_count * L, 64);
+  if (!orig || !work) {
+    free(orig);
+    free(work);
+    return -1.0;
+  }
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (size_t i = 0; i < k * shard_bytes; i++) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    orig[i] = (uint8_t)x;
+  }
+  struct timespec a, b;
+  double total = 0;
+  for (uint64_t it = 0; it < iters; it++) {
+    memset(work, 0, work_count * L * 64); /* Shards.init zeroes (untimed) */
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (uint64_t i = 0; i < k; i++) insert_shard(SHARD(work, L, i), orig + i * shard_bytes, shard_bytes);
+    encode_work(work, L, k, m, quirks);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    total += (double)(b.tv_sec - a.tv_sec) * 1e9 + (double)(b.tv_nsec - a.tv_nsec);
+  }
+  free(orig);
+  free(work);
+  return total / (double)iters;
 }

@@ -108,6 +108,9 @@ int rso_reconstruct_batch(uint64_t k, uint64_t m, size_t shard_bytes, size_t n_s
 int rso_have_avx2(void);
 void rso_force_scalar(int on);
 
+/* benchmarks.zig protocol (mean ns per insert + encode), natively timed */
+double rso_bench_encode(uint64_t k, uint64_t m, size_t shard_bytes, uint64_t iters, int quirks);
+
 #ifdef __cplusplus
 }
 #endif
