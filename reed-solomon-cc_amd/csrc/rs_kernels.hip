@@ -245,6 +245,123 @@ __device__ __forceinline__ void fft4x4(Sym<NV> *c, const RsTab *g) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// ---- the same encode with each chunk's 63 twiddle tables staged in LDS and read
+// back as VGPRs (broadcast ds_read_b128): no SGPR->VGPR moves for the v_perm
+// operands and no SGPR spills (k_encode_ws64 holds 3 x 21-SGPR tables and spills
+// ~120 SGPRs to VGPR lanes).
+__device__ __forceinline__ Tab lds_tab(const uint4 *t) {  // one RsTab = 6 x uint4
+  const uint4 q0 = t[0], q1 = t[1], q2 = t[2], q3 = t[3], q4 = t[4], q5 = t[5];
+  Tab r;
+  const uint32_t lo[10] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y};
+  const uint32_t hi[10] = {q2.z, q2.w, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    r.lo[i] = lo[i];
+    r.hi[i] = hi[i];
+  }
+  r.flags = __builtin_amdgcn_readfirstlane(q5.x);  // uniform: scalar branch on XOR-only twiddles
+  return r;
+}
+
+// group tables in plan order m01, m02, m23 (push_ifft_tabs / push_fft_tabs)
+template <int NV>
+__device__ __forceinline__ void ifft4l(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<NV> &s3, const uint4 *g) {
+  const Tab m01 = lds_tab(g), m02 = lds_tab(g + 6), m23 = lds_tab(g + 12);
+  dev::ifft_bf(s0, s1, m01);
+  dev::ifft_bf(s2, s3, m23);
+  dev::ifft_bf(s0, s2, m02);
+  dev::ifft_bf(s1, s3, m02);
+}
+
+template <int NV>
+__device__ __forceinline__ void fft4l(Sym<NV> &s0, Sym<NV> &s1, Sym<NV> &s2, Sym<NV> &s3, const uint4 *g) {
+  const Tab m01 = lds_tab(g), m02 = lds_tab(g + 6), m23 = lds_tab(g + 12);
+  dev::fft_bf(s0, s2, m02);
+  dev::fft_bf(s1, s3, m02);
+  dev::fft_bf(s0, s1, m01);
+  dev::fft_bf(s2, s3, m23);
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_ws64l(EncodeArgs a) {
+  constexpr int TI = 63;  // ifft_tab_count(64) == fft_tab_count(64)
+  __shared__ LdsSym<NV> lds[64][64];
+  __shared__ uint4 tl[TI * 6];
+  const uint64_t sb = a.shard_bytes;
+  const uint64_t regions = sb / 64 * (8 / NV) / 64;
+  if (blockIdx.x >= regions) return;  // whole block: every wave shares the region
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
+  auto stage = [&](const RsTab *src) {
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+    for (uint32_t q = threadIdx.x; q < TI * 6; q += kBlock) tl[q] = s4[q];
+  };
+  const uint64_t s = blockIdx.y;
+  const uint8_t *src = a.data + s * a.data_stripe_stride;
+  Sym<NV> acc[16];
+#pragma unroll
+  for (int u = 0; u < 16; u++) dev::zero(acc[u]);
+  for (uint32_t c = 0; c < a.n_chunks; c++) {
+    const uint32_t t = c == 0 ? a.trunc_first : (c + 1 == a.n_chunks ? a.trunc_last : 64u);
+    __syncthreads();  // previous chunk's readers of tl and lds are done
+    stage(a.tabs + static_cast<uint64_t>(c) * TI);
+    Sym<NV> cur[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {  // layout A
+      const uint32_t pos = 16 * w + j;
+      if (pos < t && !skipped(a, c * 64 + pos))
+        dev::load_sym(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
+      else dev::zero(cur[j]);
+    }
+    __syncthreads();  // tables staged
+#pragma unroll
+    for (int g = 0; g < 4; g++) {  // stage d=1, groups r = 16w + 4g
+      const uint32_t r = 16 * w + 4 * g;
+      if (r < t) ifft4l(cur[4 * g], cur[4 * g + 1], cur[4 * g + 2], cur[4 * g + 3], tl + (r / 4 * 3) * 6);
+    }
+    if (16 * w < t) {  // stage d=4, group r = 16w
+#pragma unroll
+      for (int i = 0; i < 4; i++) ifft4l(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tl + (48 + w * 3) * 6);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) lds_put(lds[16 * w + j], lane, cur[j]);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; u++) lds_get(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, cur[u]);  // layout B
+#pragma unroll
+    for (int i = 0; i < 4; i++) ifft4l(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tl + 60 * 6);  // d=16
+#pragma unroll
+    for (int u = 0; u < 16; u++) dev::xor_into(acc[u], cur[u]);  // root.zig:153-155
+  }
+  // FFT(0, 64, trunc m) on acc, root.zig:169
+  __syncthreads();
+  stage(a.tabs + static_cast<uint64_t>(a.n_chunks) * TI);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; i++) fft4l(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tl);  // d=16 (layout B)
+#pragma unroll
+  for (int u = 0; u < 16; u++) lds_put(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, acc[u]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; j++) lds_get(lds[16 * w + j], lane, acc[j]);  // layout A
+  if (16 * w < a.m) {  // d=4, group r = 16w
+#pragma unroll
+    for (int i = 0; i < 4; i++) fft4l(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tl + (3 + w * 3) * 6);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; g++) {  // d=1, groups r = 16w + 4g
+    const uint32_t r = 16 * w + 4 * g;
+    if (r < a.m) fft4l(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3], tl + (15 + r / 4 * 3) * 6);
+  }
+  uint8_t *dst = a.parity + s * a.parity_stripe_stride;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t pos = 16 * w + j;
+    if (pos < a.m) dev::store_sym(dst + pos * sb, off, acc[j], a.contig);
+  }
+}
+
 template <int NV, bool SHARED>
 __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
   constexpr int TI = 63;  // ifft_tab_count(64): 16 + 4 + 1 groups x 3
@@ -1139,7 +1256,13 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
     const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
     const char *ev = getenv("RS_AMD_WS64_SHARED");  // A/B switch: 1 (default) shared stage tables
     const bool shared = !(ev && ev[0] == '0');
-    if (kc.nv == 1) {
+    // A/B switch, default off: LDS-staged VGPR tables measured 10.2 vs 9.3 ms (NV=1,
+    // occupancy 5 -> 3 waves/SIMD at 151 VGPRs) and 10.0 vs 10.7 ms (NV=2) on RS(200,55)
+    const char *el = getenv("RS_AMD_WS64_LDS");
+    if (el && el[0] == '1') {
+      if (kc.nv == 1) hipLaunchKernelGGL((k_encode_ws64l<1>), g, dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL((k_encode_ws64l<2>), g, dim3(kBlock), 0, s, a);
+    } else if (kc.nv == 1) {
       if (shared) hipLaunchKernelGGL((k_encode_ws64<1, true>), g, dim3(kBlock), 0, s, a);
       else hipLaunchKernelGGL((k_encode_ws64<1, false>), g, dim3(kBlock), 0, s, a);
     } else {
