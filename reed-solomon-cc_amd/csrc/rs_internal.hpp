@@ -71,6 +71,12 @@ struct DecodeArgs {
   // (xsrc = the encode of the received data, [stripe][m][shard_bytes])
   const uint8_t *xsrc = nullptr;
   uint64_t xsrc_stripe_stride = 0;
+  // matrix kernel with per-stripe matrices (per-stripe erasure patterns): stripe s
+  // uses tab_mat + s * mat_stride, pos_src + s * src_stride and restores nout[s]
+  // outputs (the rest of its row is not written)
+  uint64_t mat_stride = 0;
+  uint64_t src_stride = 0;
+  const int32_t *nout = nullptr;
 };
 constexpr int32_t kSrcXorScratch = 0x20000000;
 constexpr int32_t kSrcRecovery = 0x40000000;
@@ -110,6 +116,18 @@ hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride
                                uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
                                const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
                                RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s);
+
+// Per-stripe patterns as per-stripe e x k matrices (corrected multiply, W <= 32):
+// images [n][k][max_e][16] (scratch), tabs [n][k][max_e] (matrix-kernel rows),
+// srcs [n][k] (input shards), nout [n] (restored outputs per stripe)
+hipError_t launch_pattern_matrix(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                                 uint32_t W, uint64_t n, uint32_t max_e, const uint16_t *logs, const RsTab *tab_ifft,
+                                 const RsTab *tab_fft, const uint16_t *d_exp, const uint16_t *d_log, uint16_t *images,
+                                 RsTab *tabs, int32_t *srcs, int32_t *nout, hipStream_t s);
+
+// present rows trimmed to the k shards the matrix path decodes from (out: [n][k+m])
+hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
+                               uint8_t *out, hipStream_t s);
 
 // Shard tails: pack one shard's last partial chunk into / out of the padded layout
 hipError_t launch_tail_pack(const uint8_t *src, uint64_t src_stripe_stride, uint8_t *dst, uint64_t dst_stripe_stride,

@@ -341,7 +341,14 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &err) 
 bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *code_bytes) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
-  const bool ok = compile(generate(spec, kernel_name(spec, spec_key(spec, -1))), code, err);
+  const std::string name = kernel_name(spec, spec_key(spec, -1)), src = generate(spec, name);
+  if (const char *dir = std::getenv("RS_AMD_JIT_DUMP")) {  // debug aid: keep the generated source
+    if (FILE *f = std::fopen((std::string(dir) + "/" + name + ".hip").c_str(), "w")) {
+      std::fputs(src.c_str(), f);
+      std::fclose(f);
+    }
+  }
+  const bool ok = compile(src, code, err);
   if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (code_bytes) *code_bytes = code.size();
   return ok;

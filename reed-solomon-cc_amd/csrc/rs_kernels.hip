@@ -513,10 +513,12 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
   const uint64_t sb = a.shard_bytes;
   typedef const __attribute__((address_space(4))) int32_t *CI;
-  const CI srcs = (CI)(a.pos_src);
   const uint32_t n_in = a.n_in;
   {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
     const uint64_t s = blockIdx.y;
+    const CI srcs = (CI)(a.pos_src + s * a.src_stride);
+    const RsTab *mat = a.tab_mat + s * a.mat_stride;
+    const uint32_t e_s = a.nout ? static_cast<uint32_t>(((CI)(a.nout))[s]) : static_cast<uint32_t>(E);
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
     const uint8_t *xs = a.xsrc + s * a.xsrc_stripe_stride;
@@ -533,7 +535,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
         if (i + 1 < n_in) load_in(nxt, i + 1);
         Sel<NV> sel;
         make_sel(sel, y);
-        const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * E;
+        const RsTab *row = mat + static_cast<uint64_t>(i) * E;
 #pragma unroll
         for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
         y = nxt;
@@ -550,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
           if (i0 + d >= n_in) break;
           Sel<NV> sel;
           make_sel(sel, y[d]);
-          const RsTab *row = a.tab_mat + static_cast<uint64_t>(i0 + d) * E;
+          const RsTab *row = mat + static_cast<uint64_t>(i0 + d) * E;
 #pragma unroll
           for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
         }
@@ -558,7 +560,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     }
     uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
-    for (int j = 0; j < E; j++) dev::store_sym(out + static_cast<uint64_t>(j) * sb, off, acc[j], a.contig);
+    for (int j = 0; j < E; j++)
+      if (static_cast<uint32_t>(j) < e_s) dev::store_sym(out + static_cast<uint64_t>(j) * sb, off, acc[j], a.contig);
   }
 }
 
@@ -1011,6 +1014,206 @@ __global__ __launch_bounds__(256) void k_pattern_tables(const uint8_t *__restric
   dst[g] = dv;
 }
 
+// ---- per-stripe patterns as per-stripe e x k matrices (corrected multiply)
+// One thread per (stripe, input t, basis bit b): the reconstruct of root.zig:268-335
+// on one symbol per position (W <= 32 in registers), input t = basis symbol 1 << b,
+// every other position zero; the restored originals are column (t, b) of the
+// stripe's map. Inputs: the present originals, then the first e present recovery
+// shards (k in all); outputs: the missing originals, ascending, up to max_e.
+__device__ __forceinline__ void ifft_bf_s(uint32_t &x, uint32_t &y, const RsTab &t, const uint16_t *exp,
+                                          const uint16_t *log) {
+  y ^= x;
+  if (!(t.flags & kTabXorOnly)) x ^= mul16_d(y, t.log_m, exp, log);
+}
+__device__ __forceinline__ void fft_bf_s(uint32_t &x, uint32_t &y, const RsTab &t, const uint16_t *exp,
+                                         const uint16_t *log) {
+  if (!(t.flags & kTabXorOnly)) x ^= mul16_d(y, t.log_m, exp, log);
+  y ^= x;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void k_pattern_images(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                        uint32_t k, uint32_t m, uint32_t C, uint64_t n, uint32_t max_e,
+                                                        const uint16_t *__restrict__ logs, const RsTab *__restrict__ ti,
+                                                        const RsTab *__restrict__ tf, const uint16_t *__restrict__ exp,
+                                                        const uint16_t *__restrict__ log, uint16_t *__restrict__ images,
+                                                        int32_t *__restrict__ srcs, int32_t *__restrict__ nout) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= n * k * 16) return;
+  const uint64_t s = g / (k * 16);
+  const uint32_t t = static_cast<uint32_t>(g / 16 % k), b = static_cast<uint32_t>(g % 16);
+  const uint8_t *pr = present + s * present_stride;
+  const uint16_t *lg = logs + s * W;
+  uint32_t have = 0, e = 0;
+  for (uint32_t i = 0; i < k + m; i++) have += pr[i] ? 1 : 0;
+  for (uint32_t i = 0; i < k; i++) e += pr[i] ? 0 : 1;
+  int32_t in_pos = -1, src = 0;
+  uint32_t cnt = 0;
+  for (uint32_t i = 0; i < k && in_pos < 0; i++)
+    if (pr[i]) {
+      if (cnt == t) in_pos = static_cast<int32_t>(C + i), src = static_cast<int32_t>(i);
+      cnt++;
+    }
+  for (uint32_t r = 0; r < m && in_pos < 0; r++)
+    if (pr[k + r]) {
+      if (cnt == t) in_pos = static_cast<int32_t>(r), src = kSrcRecovery | static_cast<int32_t>(r);
+      cnt++;
+    }
+  if (b == 0) srcs[s * k + t] = src;  // a valid shard even for NotEnoughShards stripes (nothing is stored)
+  if (t == 0 && b == 0) nout[s] = have >= k ? static_cast<int32_t>(min(e, max_e)) : 0;
+  const uint32_t trunc = C + k;
+  uint32_t v[W];
+  const uint32_t x0 = in_pos >= 0 ? mul16_d(1u << b, lg[in_pos], exp, log) : 0u;  // erasure mask, root.zig:291-302
+#pragma unroll
+  for (int p = 0; p < W; p++) v[p] = p == in_pos ? x0 : 0u;
+  {  // IFFT, Generic.zig:80-147 (schedule of push_ifft_tabs)
+    int q = 0, d = 1;
+#pragma unroll
+    for (int d4 = 4; d4 <= W; d4 <<= 2) {
+#pragma unroll
+      for (int r = 0; r < W; r += d4) {
+        if (static_cast<uint32_t>(r) < trunc) {
+          const RsTab m01 = ti[q], m02 = ti[q + 1], m23 = ti[q + 2];
+#pragma unroll
+          for (int i = r; i < r + d; i++) {
+            ifft_bf_s(v[i], v[i + d], m01, exp, log);
+            ifft_bf_s(v[i + 2 * d], v[i + 3 * d], m23, exp, log);
+            ifft_bf_s(v[i], v[i + 2 * d], m02, exp, log);
+            ifft_bf_s(v[i + d], v[i + 3 * d], m02, exp, log);
+          }
+        }
+        q += 3;
+      }
+      d = d4;
+    }
+    if (d < W) {
+#pragma unroll
+      for (int i = 0; i < d; i++) ifft_bf_s(v[i], v[d + i], ti[q], exp, log);
+    }
+  }
+#pragma unroll
+  for (int i = 1; i < W; i++) {  // formal derivative, root.zig:309-315
+    const int w = i & -i;
+#pragma unroll
+    for (int j = 0; j < w; j++)
+      if (i + j < W) v[i - w + j] ^= v[i + j];
+  }
+  {  // FFT, Generic.zig:15-78 (schedule of push_fft_tabs)
+    int q = 0, d4 = W;
+#pragma unroll
+    for (int d = W >> 2; d != 0; d >>= 2) {
+#pragma unroll
+      for (int r = 0; r < W; r += d4) {
+        if (static_cast<uint32_t>(r) < trunc) {
+          const RsTab m01 = tf[q], m02 = tf[q + 1], m23 = tf[q + 2];
+#pragma unroll
+          for (int i = r; i < r + d; i++) {
+            fft_bf_s(v[i], v[i + 2 * d], m02, exp, log);
+            fft_bf_s(v[i + d], v[i + 3 * d], m02, exp, log);
+            fft_bf_s(v[i], v[i + d], m01, exp, log);
+            fft_bf_s(v[i + 2 * d], v[i + 3 * d], m23, exp, log);
+          }
+        }
+        q += 3;
+      }
+      d4 = d;
+    }
+    if (d4 == 2) {
+#pragma unroll
+      for (int r = 0; r < W; r += 2)
+        if (static_cast<uint32_t>(r) < trunc) fft_bf_s(v[r], v[r + 1], tf[q + r / 2], exp, log);
+    }
+  }
+  uint16_t *img = images + (s * k + t) * max_e * 16 + b;
+  uint32_t j = 0;
+#pragma unroll
+  for (int p = 0; p < W; p++) {  // reveal the missing originals, root.zig:320-326
+    if (static_cast<uint32_t>(p) >= C && static_cast<uint32_t>(p) < C + k && !pr[p - C]) {
+      if (j < max_e) img[j * 16] = static_cast<uint16_t>(mul16_d(v[p], 65535u - lg[p], exp, log));
+      j++;
+    }
+  }
+  for (; j < max_e; j++) img[j * 16] = 0;
+}
+
+// The matrix path decodes from exactly k received shards (the present originals and
+// the first e present recovery shards), so the erasure locator must be evaluated for
+// that set: present rows with the other recovery shards marked absent.
+__global__ __launch_bounds__(256) void k_trim_present(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                      uint32_t k, uint32_t m, uint64_t n, uint8_t *__restrict__ out) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint8_t *pr = present + s * present_stride;
+  uint8_t *o = out + s * (k + m);
+  uint32_t e = 0;
+  for (uint32_t i = 0; i < k; i++) {
+    o[i] = pr[i] ? 1 : 0;
+    e += pr[i] ? 0 : 1;
+  }
+  uint32_t used = 0;
+  for (uint32_t r = 0; r < m; r++) {
+    const bool keep = pr[k + r] && used < e;
+    used += keep ? 1 : 0;
+    o[k + r] = keep ? 1 : 0;
+  }
+  // fewer than k present in total: keep the row as it is (the plan reports NotEnoughShards)
+  if (used < e)
+    for (uint32_t r = 0; r < m; r++) o[k + r] = pr[k + r] ? 1 : 0;
+}
+
+// rs_gf.cpp make_tab_from_images on device: one thread per (stripe, input, output)
+__global__ __launch_bounds__(256) void k_pattern_mtabs(const uint16_t *__restrict__ images, uint64_t count,
+                                                       RsTab *__restrict__ tabs) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (g >= count) return;
+  const uint16_t *img = images + g * 16;
+  constexpr int kOff[6] = {0, 3, 6, 8, 11, 14};
+  constexpr int kBits[6] = {3, 3, 2, 3, 3, 2};
+  constexpr int kSlot[6] = {0, 2, 4, 5, 7, 9};
+  RsTab t;
+#pragma unroll
+  for (int i = 0; i < 10; i++) t.lo[i] = t.hi[i] = 0;
+#pragma unroll
+  for (int f = 0; f < 6; f++)
+    for (uint32_t v = 0; v < (1u << kBits[f]); v++) {
+      uint32_t p = 0;
+      for (int bit = 0; bit < kBits[f]; bit++)
+        if (v >> bit & 1) p ^= img[kOff[f] + bit];
+      const int w = kSlot[f] + (v >> 2), sh = 8 * (v & 3);
+      t.lo[w] |= (p & 0xFF) << sh;
+      t.hi[w] |= (p >> 8) << sh;
+    }
+  t.flags = 0;
+  t.log_m = 0;
+  t.pad[0] = t.pad[1] = 0;
+  tabs[g] = t;
+}
+
+hipError_t launch_pattern_matrix_impl(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m,
+                                      uint32_t C, uint32_t W, uint64_t n, uint32_t max_e, const uint16_t *logs,
+                                      const RsTab *tab_ifft, const RsTab *tab_fft, const uint16_t *d_exp,
+                                      const uint16_t *d_log, uint16_t *images, RsTab *tabs, int32_t *srcs,
+                                      int32_t *nout, hipStream_t s) {
+  const uint64_t threads = n * k * 16;
+  const dim3 grid(static_cast<uint32_t>((threads + 255) / 256));
+  switch (W) {
+#define RS_PIMG(W_)                                                                                                   \
+  case W_:                                                                                                            \
+    hipLaunchKernelGGL(k_pattern_images<W_>, grid, dim3(256), 0, s, d_present, present_stride, k, m, C, n, max_e, logs, \
+                       tab_ifft, tab_fft, d_exp, d_log, images, srcs, nout);                                          \
+    break;
+    RS_PIMG(2) RS_PIMG(4) RS_PIMG(8) RS_PIMG(16) RS_PIMG(32)
+#undef RS_PIMG
+    default: return hipErrorInvalidValue;
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t count = n * k * max_e;
+  hipLaunchKernelGGL(k_pattern_mtabs, dim3(static_cast<uint32_t>((count + 255) / 256)), dim3(256), 0, s, images, count,
+                     tabs);
+  return hipGetLastError();
+}
+
 hipError_t launch_pattern_plan_impl(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m,
                                     uint32_t C, uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
                                     const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
@@ -1228,6 +1431,9 @@ hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_
     b.rec += s0 * a.rec_stripe_stride;
     b.out += s0 * a.out_stripe_stride;
     if (b.xsrc) b.xsrc += s0 * a.xsrc_stripe_stride;
+    b.tab_mat += s0 * a.mat_stride;
+    b.pos_src += s0 * a.src_stride;
+    if (b.nout) b.nout += s0;
     b.tab_pre += s0 * a.pattern_stride;
     b.tab_post += s0 * a.pattern_stride;
     b.pos_src += s0 * a.pattern_stride;
@@ -1315,6 +1521,21 @@ hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride
                                RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
   return launch_pattern_plan_impl(d_present, present_stride, k, m, C, W, n, max_e, d1, d_exp, d_log, d_log_walsh,
                                   logs, pre, post, src, dst, status, s);
+}
+
+hipError_t launch_pattern_matrix(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                                 uint32_t W, uint64_t n, uint32_t max_e, const uint16_t *logs, const RsTab *tab_ifft,
+                                 const RsTab *tab_fft, const uint16_t *d_exp, const uint16_t *d_log, uint16_t *images,
+                                 RsTab *tabs, int32_t *srcs, int32_t *nout, hipStream_t s) {
+  return launch_pattern_matrix_impl(d_present, present_stride, k, m, C, W, n, max_e, logs, tab_ifft, tab_fft, d_exp,
+                                    d_log, images, tabs, srcs, nout, s);
+}
+
+hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
+                               uint8_t *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_trim_present, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, present,
+                     present_stride, k, m, n, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_tail_pack(const uint8_t *src, uint64_t src_stripe_stride, uint8_t *dst, uint64_t dst_stripe_stride,

@@ -371,8 +371,12 @@ def test_host_batch_pipeline(oracle, pinned):
 @pytest.mark.parametrize("k,m,sb", [(10, 4, 4096), (5, 5, 320), (4, 2, 2048), (16, 16, 1024), (20, 16, 512),
                                     (200, 55, 512)])
 @pytest.mark.parametrize("flags", [0, 1])
-def test_reconstruct_per_stripe_patterns(oracle, k, m, sb, flags):
-    """rs_reconstruct_batch_dev_patterns: erasure locator per stripe on the GPU (LDS FWHT)."""
+@pytest.mark.parametrize("path", ["auto", "fft"])
+def test_reconstruct_per_stripe_patterns(oracle, monkeypatch, k, m, sb, flags, path):
+    """rs_reconstruct_batch_dev_patterns: erasure locator per stripe on the GPU (LDS FWHT),
+    then per-stripe matrices built on the GPU + the matrix kernel (auto, corrected, W <= 32,
+    max_e <= 8) or the FFT reconstruct kernels (RS_AMD_PATTERNS=fft)."""
+    monkeypatch.setenv("RS_AMD_PATTERNS", path)
     n = 9
     rng = np.random.default_rng(k * 31 + m + flags)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
@@ -384,7 +388,7 @@ def test_reconstruct_per_stripe_patterns(oracle, k, m, sb, flags):
     present[n - 1, :] = 1
     present[n - 1, :m + 1] = 0  # not enough shards
     max_e = m
-    out = torch.zeros((n, max_e, sb), dtype=torch.uint8, device=DEV)
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
     status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
     R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
     torch.cuda.synchronize()
@@ -394,6 +398,7 @@ def test_reconstruct_per_stripe_patterns(oracle, k, m, sb, flags):
     for s in range(n - 1):
         assert status[s] == 0, s
         missing = [i for i in range(k) if not present[s, i]]
+        assert (out[s, len(missing):] == 0xAB).all(), s  # slots >= e_s are not written
         if not missing:
             continue
         exp = oracle.reconstruct_batch(k, m, present[s], np.concatenate([data[s:s + 1], par[s:s + 1]], axis=1),
