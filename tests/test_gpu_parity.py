@@ -423,3 +423,22 @@ def test_shard_tails_vs_oracle(oracle, k, m, sb):
     present[lost] = 0
     got = gpu_reconstruct(k, m, present, data, par)
     assert (got == data[:, sorted(lost)]).all()
+
+
+def test_more_than_65535_stripes(oracle):
+    """Launch splitting at 65535 stripes (grid y): network encode + reconstruct over
+    65,540 stripes; the stripes either side of the split are checked against the oracle."""
+    k, m, sb, n = 4, 2, 4096, 65540
+    g = torch.Generator(device=DEV)
+    g.manual_seed(65540)
+    d = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8, device=DEV, generator=g)
+    p = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p)
+    present = [0, 1, 1, 0, 1, 1]
+    out = torch.zeros((n, 2, sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, d, p, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, d[:, [0, 3]])
+    idx = [0, 65533, 65534, 65535, 65536, n - 1]
+    sample = d[idx].cpu().numpy()
+    assert (p[idx].cpu().numpy() == oracle.encode_batch(k, m, sample)).all()
