@@ -1376,29 +1376,47 @@ hipError_t copy_rows(void *dst, uint64_t dst_stride, const void *src, uint64_t s
   return hipMemcpy2DAsync(dst, dst_stride, src, src_stride, row_bytes, rows, kind, s);
 }
 
+// Per-device staging ring of the host-batch calls: kSlots slices, each on its own
+// stream (H2D -> kernel -> D2H in order; slices on different streams overlap both
+// PCIe directions with the kernels). Buffers and streams persist across calls and
+// grow on demand; the ring's mutex serialises host-batch calls on one device.
 struct Pipeline {
   static constexpr int kSlots = 3;
+  std::mutex mu;
   hipStream_t st[kSlots] = {};
   void *buf[kSlots][3] = {};
-  ~Pipeline() {
-    for (int i = 0; i < kSlots; i++) {
-      if (st[i]) (void)hipStreamSynchronize(st[i]);
-      for (void *b : buf[i])
-        if (b) (void)hipFree(b);
-      if (st[i]) (void)hipStreamDestroy(st[i]);
-    }
-  }
-  int init(const uint64_t bytes[3]) {
-    for (int i = 0; i < kSlots; i++) {
-      HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-      for (int j = 0; j < 3; j++)
-        if (bytes[j]) HIP_TRY(hipMalloc(&buf[i][j], bytes[j]));
+  uint64_t cap[3] = {};
+  int ensure(const uint64_t bytes[3]) {
+    for (int i = 0; i < kSlots; i++)
+      if (!st[i]) HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+    for (int j = 0; j < 3; j++) {
+      if (bytes[j] <= cap[j]) continue;
+      for (int i = 0; i < kSlots; i++) {
+        if (buf[i][j]) HIP_TRY(hipFree(buf[i][j]));
+        buf[i][j] = nullptr;
+      }
+      cap[j] = 0;
+      for (int i = 0; i < kSlots; i++) HIP_TRY(hipMalloc(&buf[i][j], bytes[j]));
+      cap[j] = bytes[j];
     }
     return RS_OK;
   }
   int finish() {
     for (int i = 0; i < kSlots; i++) HIP_TRY(hipStreamSynchronize(st[i]));
     return RS_OK;
+  }
+};
+
+// process-lifetime rings (never freed: the HIP runtime reclaims them at exit)
+std::mutex g_pipe_mu;
+std::map<int, Pipeline *> g_pipes;
+
+struct Pipelines {
+  static Pipeline &of(int dev) {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    Pipeline *&p = g_pipes[dev];
+    if (!p) p = new Pipeline();
+    return *p;
   }
 };
 
@@ -1418,9 +1436,10 @@ int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const vo
   int dev;
   if ((st = current_device(&dev))) return st;
   const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, kSliceBytes / (k * sb)));
-  Pipeline p;
+  Pipeline &p = Pipelines::of(dev);
+  std::lock_guard<std::mutex> lk(p.mu);
   const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
-  if ((st = p.init(bytes))) return st;
+  if ((st = p.ensure(bytes))) return st;
   for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
     const int slot = static_cast<int>(i % Pipeline::kSlots);
     const uint64_t cnt = std::min(S, n - s0);
@@ -1452,9 +1471,10 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
   int dev;
   if ((st = current_device(&dev))) return st;
   const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, kSliceBytes / (k * sb)));
-  Pipeline p;
+  Pipeline &p = Pipelines::of(dev);
+  std::lock_guard<std::mutex> lk(p.mu);
   const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
-  if ((st = p.init(bytes))) return st;
+  if ((st = p.ensure(bytes))) return st;
   for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
     const int slot = static_cast<int>(i % Pipeline::kSlots);
     const uint64_t cnt = std::min(S, n - s0);
