@@ -207,8 +207,13 @@ struct VecT<4> {
 // Measured on MI355X (tools/hbm_probe.hip): contiguous wave accesses stream ~5% faster.
 // `base` is wave-uniform (stripe/shard start) and `off` the lane's 32-bit offset,
 // so the compiler can use the SGPR-base form of global_load/store (saddr + voffset).
+// load_sym = load_sym_raw (issue the loads) + pair_halves (the contig swap, which
+// must wait for them). Kernels loading several slots issue every raw load first and
+// pair afterwards: a swap right behind its own load serialises one HBM round trip
+// per slot (s_waitcnt vmcnt(0) before each v_permlane32_swap).
 template <int NV>
-__device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__ base, uint32_t off, bool contig) {
+__device__ __forceinline__ void load_sym_raw(Sym<NV> &s, const uint8_t *__restrict__ base, uint32_t off,
+                                             bool contig) {
   typedef typename VecT<NV>::type V;
   const uint8_t *p = base + off;
   const V a = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
@@ -223,6 +228,10 @@ __device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__
       s.h[v] = b[v];
     }
   }
+}
+
+template <int NV>
+__device__ __forceinline__ void pair_halves(Sym<NV> &s, bool contig) {
   if (contig) {
 #pragma unroll
     for (int v = 0; v < NV; v++) {
@@ -231,6 +240,12 @@ __device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__
       s.h[v] = r[1];
     }
   }
+}
+
+template <int NV>
+__device__ __forceinline__ void load_sym(Sym<NV> &s, const uint8_t *__restrict__ base, uint32_t off, bool contig) {
+  load_sym_raw(s, base, off, contig);
+  pair_halves(s, contig);
 }
 
 template <int NV>

@@ -72,9 +72,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
 #pragma unroll
     for (int p = 0; p < C; p++) {
       if (static_cast<uint32_t>(p) < a.trunc_first && !skipped(a, p))
-        dev::load_sym(acc[p], src + p * sb, off, a.contig);
+        dev::load_sym_raw(acc[p], src + p * sb, off, a.contig);
       else dev::zero(acc[p]);
     }
+#pragma unroll
+    for (int p = 0; p < C; p++) dev::pair_halves(acc[p], a.contig);
     dev::ifft_regs<C>(acc, a.tabs, a.trunc_first);
     // further chunks, IFFT + XOR-fold: root.zig:148-167
     for (uint32_t j = 1; j < a.n_chunks; j++) {
@@ -83,9 +85,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_reg(EncodeArgs a) {
       Sym<NV> cur[C];
 #pragma unroll
       for (int p = 0; p < C; p++) {
-        if (static_cast<uint32_t>(p) < t && !skipped(a, j * C + p)) dev::load_sym(cur[p], cs + p * sb, off, a.contig);
+        if (static_cast<uint32_t>(p) < t && !skipped(a, j * C + p)) dev::load_sym_raw(cur[p], cs + p * sb, off, a.contig);
         else dev::zero(cur[p]);
       }
+#pragma unroll
+      for (int p = 0; p < C; p++) dev::pair_halves(cur[p], a.contig);
       const RsTab *tj = a.tabs + j * TI;
       asm volatile("" : "+s"(tj));  // opaque base: no per-group pointer IVs (SGPR spills)
       dev::ifft_regs<C>(cur, tj, t);
@@ -132,10 +136,16 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
       const int32_t src = ((const __attribute__((address_space(4))) int32_t *)pos_src)[p];
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, off, a.contig);
-        dev::mul_inplace(w[p], dev::load_tab(tab_pre + p));
+        dev::load_sym_raw(w[p], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, off, a.contig);
       } else {
         dev::zero(w[p]);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < W; p++) {  // all loads in flight before the first swap waits
+      if (((const __attribute__((address_space(4))) int32_t *)pos_src)[p] >= 0) {
+        dev::pair_halves(w[p], a.contig);
+        dev::mul_inplace(w[p], dev::load_tab(tab_pre + p));
       }
     }
     dev::ifft_regs<W>(w, a.tab_ifft, a.trunc);  // root.zig:306
@@ -311,9 +321,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64l(EncodeArgs a) {
     for (int j = 0; j < 16; j++) {  // layout A
       const uint32_t pos = 16 * w + j;
       if (pos < t && !skipped(a, c * 64 + pos))
-        dev::load_sym(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
+        dev::load_sym_raw(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
       else dev::zero(cur[j]);
     }
+#pragma unroll
+    for (int j = 0; j < 16; j++) dev::pair_halves(cur[j], a.contig);
     __syncthreads();  // tables staged
 #pragma unroll
     for (int g = 0; g < 4; g++) {  // stage d=1, groups r = 16w + 4g
@@ -387,9 +399,11 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
       for (int j = 0; j < 16; j++) {  // layout A
         const uint32_t pos = 16 * w + j;
         if (pos < t && !skipped(a, c * 64 + pos))
-          dev::load_sym(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
+          dev::load_sym_raw(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
         else dev::zero(cur[j]);
       }
+#pragma unroll
+      for (int j = 0; j < 16; j++) dev::pair_halves(cur[j], a.contig);
 #pragma unroll
       for (int g = 0; g < 4; g++) {  // stage d=1, groups r = 16w + 4g
         const uint32_t r = 16 * w + 4 * g;
@@ -495,16 +509,37 @@ __device__ __forceinline__ void mac_sel(Sym<NV> &x, const Sel<NV> &s, const Tab 
 
 // One received input of the matrix kernels: orig[idx] or rec[idx]; with
 // kSrcXorScratch, rec[idx] ^ xs[idx] (a syndrome, reconstruct by syndromes).
+// Split in two so a prefetched input keeps its loads in flight: issue_input only
+// issues them, take_input waits, XORs the syndrome part and pairs the lane halves
+// (the swap is a lane permutation, so it commutes with the XOR).
+template <int NV>
+struct InFlight {
+  Sym<NV> y, z;
+  bool x;
+};
+
+template <int NV>
+__device__ __forceinline__ void issue_input(InFlight<NV> &f, int32_t src, const uint8_t *orig, const uint8_t *rec,
+                                            const uint8_t *xs, uint64_t sb, uint32_t off, bool contig) {
+  const uint64_t o = static_cast<uint64_t>(src & kSrcIndexMask) * sb;
+  dev::load_sym_raw(f.y, ((src & kSrcRecovery) ? rec : orig) + o, off, contig);
+  f.x = (src & kSrcXorScratch) != 0;
+  if (f.x) dev::load_sym_raw(f.z, xs + o, off, contig);
+}
+
+template <int NV>
+__device__ __forceinline__ void take_input(Sym<NV> &y, const InFlight<NV> &f, bool contig) {
+  y = f.y;
+  if (f.x) dev::xor_into(y, f.z);
+  dev::pair_halves(y, contig);
+}
+
 template <int NV>
 __device__ __forceinline__ void load_input(Sym<NV> &y, int32_t src, const uint8_t *orig, const uint8_t *rec,
                                            const uint8_t *xs, uint64_t sb, uint32_t off, bool contig) {
-  const uint64_t o = static_cast<uint64_t>(src & kSrcIndexMask) * sb;
-  dev::load_sym(y, ((src & kSrcRecovery) ? rec : orig) + o, off, contig);
-  if (src & kSrcXorScratch) {
-    Sym<NV> z;
-    dev::load_sym(z, xs + o, off, contig);
-    dev::xor_into(y, z);
-  }
+  InFlight<NV> f;
+  issue_input(f, src, orig, rec, xs, sb, off, contig);
+  take_input(y, f, contig);
 }
 
 template <int E, int NV, int D>
@@ -522,36 +557,38 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
     const uint8_t *xs = a.xsrc + s * a.xsrc_stripe_stride;
-    auto load_in = [&](Sym<NV> &y, uint32_t i) { load_input(y, srcs[i], orig, rec, xs, sb, off, a.contig); };
+    auto issue = [&](InFlight<NV> &f, uint32_t i) { issue_input(f, srcs[i], orig, rec, xs, sb, off, a.contig); };
     Sym<NV> acc[E];
 #pragma unroll
     for (int j = 0; j < E; j++) dev::zero(acc[j]);
     if constexpr (D == 1) {
       // one input ahead: input i+1 in flight while input i is multiplied
-      Sym<NV> y;
-      load_in(y, 0);
+      InFlight<NV> f;
+      issue(f, 0);
       for (uint32_t i = 0; i < n_in; i++) {
-        Sym<NV> nxt = y;
-        if (i + 1 < n_in) load_in(nxt, i + 1);
+        Sym<NV> y;
+        take_input(y, f, a.contig);
+        if (i + 1 < n_in) issue(f, i + 1);
         Sel<NV> sel;
         make_sel(sel, y);
         const RsTab *row = mat + static_cast<uint64_t>(i) * E;
 #pragma unroll
         for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
-        y = nxt;
       }
     } else {
       // batches of D inputs: D loads in flight together, then D x E MACs
       for (uint32_t i0 = 0; i0 < n_in; i0 += D) {
-        Sym<NV> y[D];
+        InFlight<NV> f[D];
 #pragma unroll
         for (int d = 0; d < D; d++)
-          if (i0 + d < n_in) load_in(y[d], i0 + d);
+          if (i0 + d < n_in) issue(f[d], i0 + d);
 #pragma unroll
         for (int d = 0; d < D; d++) {
           if (i0 + d >= n_in) break;
+          Sym<NV> y;
+          take_input(y, f[d], a.contig);
           Sel<NV> sel;
-          make_sel(sel, y[d]);
+          make_sel(sel, y);
           const RsTab *row = mat + static_cast<uint64_t>(i0 + d) * E;
 #pragma unroll
           for (int j = 0; j < E; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
@@ -589,18 +626,18 @@ __global__ __launch_bounds__(kBlock) void k_decode_mtile(DecodeArgs a) {
   Sym<NV> acc[EW];
 #pragma unroll
   for (int j = 0; j < EW; j++) dev::zero(acc[j]);
-  Sym<NV> y;
-  load_input(y, srcs[0], orig, rec, xs, sb, off, a.contig);
+  InFlight<NV> f;
+  issue_input(f, srcs[0], orig, rec, xs, sb, off, a.contig);
   for (uint32_t i = 0; i < a.n_in; i++) {
-    Sym<NV> nxt = y;
-    if (i + 1 < a.n_in) load_input(nxt, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
+    Sym<NV> y;
+    take_input(y, f, a.contig);
+    if (i + 1 < a.n_in) issue_input(f, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
     Sel<NV> sel;
     make_sel(sel, y);
     const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * stride + j0;
     asm volatile("" : "+s"(row));
 #pragma unroll
     for (int j = 0; j < EW; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
-    y = nxt;
   }
   uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
@@ -655,13 +692,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_mtile_lds(DecodeArgs a) {
   for (int j = 0; j < EW; j++) dev::zero(acc[j]);
   stage(0, 0);
   __syncthreads();
-  Sym<NV> y;
-  if (nj) load_input(y, srcs[0], orig, rec, xs, sb, off, a.contig);
+  InFlight<NV> f;
+  if (nj) issue_input(f, srcs[0], orig, rec, xs, sb, off, a.contig);
   for (uint32_t i = 0; i < a.n_in; i++) {
-    Sym<NV> nxt = y;
+    Sym<NV> y;
+    if (nj) take_input(y, f, a.contig);
     if (i + 1 < a.n_in) {
       stage(i + 1, (i + 1) & 1);
-      if (nj) load_input(nxt, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
+      if (nj) issue_input(f, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
     }
     if (nj) {
       Sel<NV> sel;
@@ -678,7 +716,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_mtile_lds(DecodeArgs a) {
       }
     }
     __syncthreads();  // buffer (i & 1) free for input i + 2
-    y = nxt;
   }
   uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
