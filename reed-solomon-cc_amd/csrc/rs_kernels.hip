@@ -374,7 +374,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64l(EncodeArgs a) {
   }
 }
 
-template <int NV, bool SHARED>
+// PF: chunk c+1's loads are issued right after chunk c's are paired, so they are in
+// flight during chunk c's butterflies and LDS transposes (+16 dword pairs per lane).
+template <int NV, bool SHARED, bool PF>
 __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
   constexpr int TI = 63;  // ifft_tab_count(64): 16 + 4 + 1 groups x 3
   __shared__ LdsSym<NV> lds[64][64];
@@ -387,23 +389,37 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
   {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
     const uint64_t s = blockIdx.y;
     const uint8_t *src = a.data + s * a.data_stripe_stride;
-    Sym<NV> acc[16];
+    auto trunc_of = [&](uint32_t c) { return c == 0 ? a.trunc_first : (c + 1 == a.n_chunks ? a.trunc_last : 64u); };
+    auto issue_chunk = [&](Sym<NV> *d, uint32_t c) {  // layout A: wave w holds positions 16w + j
+      const uint32_t t = trunc_of(c);
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t pos = 16 * w + j;
+        if (pos < t && !skipped(a, c * 64 + pos))
+          dev::load_sym_raw(d[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
+        else dev::zero(d[j]);
+      }
+    };
+    Sym<NV> acc[16], nxt[16];
 #pragma unroll
     for (int u = 0; u < 16; u++) dev::zero(acc[u]);
+    if constexpr (PF) issue_chunk(nxt, 0);
     for (uint32_t c = 0; c < a.n_chunks; c++) {
-      const uint32_t t = c == 0 ? a.trunc_first : (c + 1 == a.n_chunks ? a.trunc_last : 64u);
+      const uint32_t t = trunc_of(c);
       const RsTab *tc = a.tabs + c * TI;
       asm volatile("" : "+s"(tc));  // opaque base: no per-group pointer IVs (SGPR spills)
       Sym<NV> cur[16];
+      if constexpr (PF) {
 #pragma unroll
-      for (int j = 0; j < 16; j++) {  // layout A
-        const uint32_t pos = 16 * w + j;
-        if (pos < t && !skipped(a, c * 64 + pos))
-          dev::load_sym_raw(cur[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
-        else dev::zero(cur[j]);
+        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
+      } else {
+        issue_chunk(cur, c);
       }
 #pragma unroll
       for (int j = 0; j < 16; j++) dev::pair_halves(cur[j], a.contig);
+      if constexpr (PF) {
+        if (c + 1 < a.n_chunks) issue_chunk(nxt, c + 1);
+      }
 #pragma unroll
       for (int g = 0; g < 4; g++) {  // stage d=1, groups r = 16w + 4g
         const uint32_t r = 16 * w + 4 * g;
@@ -1505,12 +1521,17 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
     if (el && el[0] == '1') {
       if (kc.nv == 1) hipLaunchKernelGGL((k_encode_ws64l<1>), g, dim3(kBlock), 0, s, a);
       else hipLaunchKernelGGL((k_encode_ws64l<2>), g, dim3(kBlock), 0, s, a);
-    } else if (kc.nv == 1) {
-      if (shared) hipLaunchKernelGGL((k_encode_ws64<1, true>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((k_encode_ws64<1, false>), g, dim3(kBlock), 0, s, a);
     } else {
-      if (shared) hipLaunchKernelGGL((k_encode_ws64<2, true>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((k_encode_ws64<2, false>), g, dim3(kBlock), 0, s, a);
+      // A/B switch RS_AMD_WS64_PF (next-chunk prefetch): default on for NV=2 only.
+      // RS(200,55) 256 KiB x 256: NV=1 7.57 (off) vs 7.92 ms (on, 87 -> 119 VGPRs);
+      // NV=2 14.6 vs 11.5 ms (profiles/r01/sweep_rs200_55_ws64_pf.jsonl)
+      const char *ep = getenv("RS_AMD_WS64_PF");
+      const bool pf = ep && ep[0] ? ep[0] == '1' : kc.nv == 2;
+#define RS_WS64(NV_, SH_, PF_) \
+  if (kc.nv == NV_ && shared == SH_ && pf == PF_) hipLaunchKernelGGL((k_encode_ws64<NV_, SH_, PF_>), g, dim3(kBlock), 0, s, a);
+      RS_WS64(1, true, true) RS_WS64(1, true, false) RS_WS64(1, false, true) RS_WS64(1, false, false)
+      RS_WS64(2, true, true) RS_WS64(2, true, false) RS_WS64(2, false, true) RS_WS64(2, false, false)
+#undef RS_WS64
     }
     return hipGetLastError();
   }
