@@ -175,7 +175,8 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //   RS_AMD_NET_PREFETCH  inputs loaded ahead of the one being transformed (default 0;
 //                        the compiler hoists the loads anyway)
 //   RS_AMD_NET_WAVES     amdgpu_waves_per_eu occupancy hint, 0 = none (default 0)
-//   RS_AMD_NET_NT        non-temporal loads (bit 0) / stores (bit 1), default 3
+//   RS_AMD_NET_NT        non-temporal loads (bit 0) / stores (bit 1), default 3 for
+//                        one output tile, 2 for several (their inputs are re-read)
 //   RS_AMD_NET_UNITS     4 KiB units per wave, walked in a loop (default 1)
 //   RS_AMD_NET_BARRIER   sched_barrier between inputs: bounds the scheduling regions,
 //                        so compile time stays ~linear in size (1 on, 0 off, default
@@ -218,16 +219,22 @@ std::string generate(const NetSpec &spec, const std::string &name) {
   const uint32_t n_tiles = (n_out + kTileOut - 1) / kTileOut;
   const Tuning tu = tuning();
   std::ostringstream o;
-  o << "#define RS_NT " << tu.nt << "\n" << kPrelude;
+  // several output tiles re-read every input through L2: non-temporal loads (which
+  // evict early) cost 10-15 % there, so by default they are kept for 1-tile maps only
+  const int nt = std::getenv("RS_AMD_NET_NT") || n_tiles == 1 ? tu.nt : (tu.nt & 2);
+  o << "#define RS_NT " << nt << "\n" << kPrelude;
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
   if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
   o << "void " << name
     << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
        "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0) {\n"
        "  const u32 lane = threadIdx.x & 63;\n"
-    << "  const u32 tile = blockIdx.x % " << n_tiles << "u;\n"
-    << "  const u64 ubase = ((u64)(blockIdx.x / " << n_tiles << "u) * 4 + (threadIdx.x >> 6)) * " << tu.units
-    << "u;\n"
+    // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (each with its own
+    // L2), so the n_tiles workgroups of one unit group sit 8 apart in blockIdx.x (same
+    // XCD, dispatched back to back): their input reads after the first hit that L2
+    << "  const u32 bx = blockIdx.x, tile = (bx / 8u) % " << n_tiles << "u;\n"
+    << "  const u64 ugroup = (u64)(bx / 8u / " << n_tiles << "u) * 8u + (bx % 8u);\n"
+    << "  const u64 ubase = (ugroup * 4 + (threadIdx.x >> 6)) * " << tu.units << "u;\n"
        "  const u32 ll = lane & 31;\n"
        "  const u64 s = stripe0 + blockIdx.y;\n"
        "  const unsigned char *B0 = b0 + s * s0;\n"
@@ -404,7 +411,10 @@ hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const 
                   uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s) {
   const uint64_t units = shard_bytes / kUnitBytes;
   const uint64_t per_block = 4ull * k.units;
-  const uint32_t gx = static_cast<uint32_t>((units + per_block - 1) / per_block * k.n_tiles);
+  // unit groups padded to a multiple of 8 (one per XCD, see generate()); the padding
+  // workgroups find no unit and exit
+  const uint64_t groups = (units + per_block - 1) / per_block;
+  const uint32_t gx = static_cast<uint32_t>((k.n_tiles > 1 ? (groups + 7) / 8 * 8 : groups) * k.n_tiles);
   for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
     const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
     const unsigned char *a0 = buf0, *a1 = buf1 ? buf1 : buf0;
