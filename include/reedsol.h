@@ -169,6 +169,13 @@ const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_cou
 const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                        const uint8_t *present);
 
+/* Large network maps (the e x e syndrome map of wide codes, e.g. RS(200,55) losing 55
+ * data shards: ~16-36 s of hipRTC) compile in a background thread; until they are
+ * ready the plan runs its table kernel (same bytes). rs_net_wait blocks until no such
+ * compile is running — a service can warm a pattern with one call + rs_net_wait.
+ * RS_AMD_JIT_SYNC=1 compiles them in the calling thread instead. Returns RS_OK. */
+int rs_net_wait(void);
+
 /* Plan-time network kernel: generate the bit-sliced network of an encode (present
  * == NULL) or of one reconstruct pattern and compile it with hipRTC for gfx950, without
  * loading it (no device needed: a build check). *compile_ms (optional) = compile time.

@@ -120,8 +120,15 @@ struct DevBuf {
 struct NetSlot {
   std::mutex mu;
   bool failed = false;
+  bool async = false;  // past the synchronous size cap: compiled in the background
+  uint32_t uses = 0;   // async: the compile starts at the RS_AMD_NET_ASYNC_AFTER-th use (default 2)
   jit::NetSpec spec;
 };
+
+uint32_t async_after() {
+  const char *e = std::getenv("RS_AMD_NET_ASYNC_AFTER");
+  return e && *e ? static_cast<uint32_t>(std::max(1, std::atoi(e))) : 2u;
+}
 
 struct EncodePlan {
   std::shared_ptr<DevBuf> buf;
@@ -145,12 +152,18 @@ struct DecodePlan {
 // Compile (once) and return the plan's network kernel; nullptr if hipRTC failed
 // (the caller then runs the precompiled table-driven kernels).
 // (jit::get caches by content and code-shape knobs; a failure is reported once per plan.)
+// An async slot returns nullptr (table kernels) until its background compile is done.
 const jit::Kernel *net_kernel(NetSlot &slot) {
   std::lock_guard<std::mutex> lk(slot.mu);
   if (slot.failed) return nullptr;
   std::string err;
-  const jit::Kernel *k = jit::get(slot.spec, err);
-  if (!k) {
+  bool pending = false;
+  if (slot.async && slot.uses < async_after()) {  // a one-off pattern is not worth a background compile
+    const char *sync = std::getenv("RS_AMD_JIT_SYNC");
+    if (!(sync && *sync && std::strcmp(sync, "0") != 0) && ++slot.uses < async_after()) return nullptr;
+  }
+  const jit::Kernel *k = slot.async ? jit::get_async(slot.spec, err, pending) : jit::get(slot.spec, err);
+  if (!k && !pending) {
     slot.failed = true;
     std::fprintf(stderr, "[rs_amd] bit-sliced network unavailable, using table kernels: %s\n", err.c_str());
   }
@@ -239,7 +252,8 @@ void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *pres
 // root.zig:136-173 chunk schedule -> table block
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out) {
   char key[128];
-  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u", dev, (unsigned long long)k, (unsigned long long)m, flags);
+  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu", dev, (unsigned long long)k, (unsigned long long)m, flags,
+                static_cast<unsigned long long>(jit::max_blocks()));
   std::lock_guard<std::mutex> lk(g_plan_mu);
   auto it = g_enc_plans.find(key);
   if (it != g_enc_plans.end()) {
@@ -417,7 +431,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
-                    std::to_string(jit::enabled() && sb % jit::kUnitBytes == 0 && sb < (1ull << 32)) + "/";
+                    std::to_string(jit::enabled() && sb % jit::kUnitBytes == 0 && sb < (1ull << 32)) + "/" +
+                    std::to_string(jit::max_blocks()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::lock_guard<std::mutex> lk(g_plan_mu);
@@ -440,6 +455,9 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
   const bool use_syn = !use_net && syndrome_pick(k, m, e, flags, sb, mode);
   if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
+  // the syndromes' e x e map as a network too (its table kernel stays the fallback)
+  const bool syn_net = use_syn && (mode == "auto" || mode == "net" || mode == "syndrome") && jit::enabled() &&
+                       jit::supports_async(static_cast<uint32_t>(e), static_cast<uint32_t>(e), sb);
   const bool use_matrix = kind != 0;
 
   auto plan = std::make_shared<DecodePlan>();
@@ -475,8 +493,9 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     if (st) return st;
     plan->matrix = true;
     plan->tiled = kind == 2;
-    if (use_net) {
+    if (use_net || syn_net) {
       plan->net = std::make_shared<NetSlot>();
+      plan->net->async = !jit::supports(map.n_in, map.n_out, sb);
       plan->net->spec = std::move(map);
     }
     plan->e = static_cast<uint32_t>(n_out);
@@ -884,9 +903,12 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
     return net_name("reconstruct", k, e);
   if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
     thread_local std::string name;
-    name = std::string("syndrome+") + choose_encode(k, m, sb, 4).name + "+" +
-           (e <= kMatrixMaxOut ? choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name
-                               : choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name);
+    name = std::string("syndrome+") + choose_encode(k, m, sb, 4).name + "+";
+    if (jit::enabled() && jit::supports_async(static_cast<uint32_t>(e), static_cast<uint32_t>(e), sb))
+      name += net_name("syndrome", e, e);
+    else
+      name += e <= kMatrixMaxOut ? choose_decode_matrix(static_cast<uint32_t>(e), sb, 4).name
+                                 : choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;
     return name.c_str();
   }
   switch (decode_kind(k, m, flags_none(), e, have, sb)) {
@@ -894,6 +916,11 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
     case 2: return choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;
     default: return choose_decode(k, m, sb, 4).name;
   }
+}
+
+int rs_net_wait(void) {
+  jit::wait_pending();
+  return RS_OK;
 }
 
 int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_t flags, double *compile_ms) {
@@ -904,8 +931,13 @@ int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_
     uint64_t have = 0;
     for (uint64_t i = 0; i < k + m; i++) have += present[i] != 0;
     if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+    uint64_t e = 0;
+    for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
     if (is_low_rate(k, m)) {
       if ((st = low_decode_map(k, m, flags, present, spec))) return st;
+    } else if (!jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), jit::kUnitBytes) &&
+               syndrome_pick(k, m, e, flags, jit::kUnitBytes * 64, "auto")) {
+      if ((st = syndrome_map(k, m, present, spec))) return st;  // the plan's e x e map
     } else {
       reconstruct_map(k, m, flags, present, spec);
     }
@@ -914,7 +946,9 @@ int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_
   } else {
     encode_map(k, m, flags, spec);
   }
-  if (!jit::supports(spec.n_in, spec.n_out, jit::kUnitBytes)) return fail(RS_ERR_INVALID_ARGUMENT, "no network form");
+  if (!(spec.role == "syndrome" ? jit::supports_async(spec.n_in, spec.n_out, jit::kUnitBytes)
+                                 : jit::supports(spec.n_in, spec.n_out, jit::kUnitBytes)))
+    return fail(RS_ERR_INVALID_ARGUMENT, "no network form");
   std::string err;
   if (!jit::compile_check(spec, err, compile_ms, nullptr)) return fail(RS_ERR_DEVICE, err);
   return RS_OK;
@@ -1043,7 +1077,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
   }
   std::shared_ptr<DecodePlan> plan;
   if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
-  if (plan->net && max_nv == 4) {
+  if (plan->net && !plan->syndrome && max_nv == 4) {
     if (const jit::Kernel *nk = net_kernel(*plan->net)) {
       HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,
                           static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
@@ -1100,6 +1134,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     ea.work = ep->work;
     ea.contig = contig_ok(sb, ke.nv);
     ea.skip = static_cast<const uint32_t *>(plan->skip->p);
+    const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net) : nullptr;
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap * 4 / (m * sb)));
     void *scratch = nullptr;
     HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));
@@ -1117,7 +1152,13 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       db.xsrc_stripe_stride = m * sb;
       db.n_stripes = cnt;
       hipError_t err = launch_encode(ke, eb, s);
-      if (err == hipSuccess) err = launch_decode(kc, db, s);
+      if (err == hipSuccess) {
+        if (nk)
+          err = jit::launch(*nk, db.orig, orig_stride, db.rec, rec_stride, db.out, out_stride, sb, cnt, s, db.xsrc,
+                            db.xsrc_stripe_stride);
+        else
+          err = launch_decode(kc, db, s);
+      }
       if (err != hipSuccess) {
         (void)hipFreeAsync(scratch, s);
         return hip_fail(err, "syndrome reconstruct");

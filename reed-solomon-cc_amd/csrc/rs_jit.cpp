@@ -5,13 +5,17 @@
 #include <hip/hiprtc.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <sstream>
+#include <thread>
 
 #include "rs_internal.hpp"
 
@@ -65,6 +69,16 @@ __device__ __forceinline__ Raw ld(const unsigned char *p) {
   r.a1 = LDV(p + 1024);
   r.b0 = LDV(p + 2048);
   r.b1 = LDV(p + 3072);
+  return r;
+}
+// p ^ q before the plane transform (a bit permutation, so it commutes with XOR)
+__device__ __forceinline__ Raw ldx(const unsigned char *p, const unsigned char *q) {
+  Raw r = ld(p);
+  const Raw t = ld(q);
+  r.a0 ^= t.a0;
+  r.a1 ^= t.a1;
+  r.b0 ^= t.b0;
+  r.b1 ^= t.b1;
   return r;
 }
 __device__ __forceinline__ void planes(const Raw &r, u32 *P) {
@@ -208,9 +222,14 @@ std::string tuning_key(const Tuning &t) {
 
 }  // namespace
 
+uint64_t max_blocks() {
+  const int v = env_int("RS_AMD_NET_MAX_BLOCKS", 0);
+  return v > 0 ? static_cast<uint64_t>(v) : kMaxBlocks;
+}
+
 bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
   const uint64_t blocks = static_cast<uint64_t>(n_in) * ((n_out + kTileOut - 1) / kTileOut);
-  return n_in > 0 && n_out > 0 && n_out <= kMaxOut && blocks <= kMaxBlocks && shard_bytes % kUnitBytes == 0 &&
+  return n_in > 0 && n_out > 0 && n_out <= kMaxOut && blocks <= max_blocks() && shard_bytes % kUnitBytes == 0 &&
          shard_bytes < (1ull << 32);
 }
 
@@ -227,7 +246,8 @@ std::string generate(const NetSpec &spec, const std::string &name) {
   if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
   o << "void " << name
     << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
-       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0) {\n"
+       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0,\n"
+       "    const unsigned char *__restrict__ b2, u64 s2) {\n"
        "  const u32 lane = threadIdx.x & 63;\n"
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (each with its own
     // L2), so the n_tiles workgroups of one unit group sit 8 apart in blockIdx.x (same
@@ -239,16 +259,21 @@ std::string generate(const NetSpec &spec, const std::string &name) {
        "  const u64 s = stripe0 + blockIdx.y;\n"
        "  const unsigned char *B0 = b0 + s * s0;\n"
        "  const unsigned char *B1 = b1 + s * s1;\n"
+       "  const unsigned char *B2 = b2 + s * s2;\n"
        "  unsigned char *O = out + s * so;\n"
     << "#pragma unroll 1\n"
     << "  for (u32 it = 0; it < " << tu.units << "u; it++) {\n"
        "  const u64 unit = ubase + it;\n"
        "  if (unit * 4096 >= sb) break;\n"
        "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n";
-  auto in_expr = [&](uint32_t t) {
+  auto load_expr = [&](uint32_t t) {  // ld(shard) or ldx(shard, scratch) for a syndrome input
     const int32_t src = spec.src[t];
+    const uint32_t idx = static_cast<uint32_t>(src & kSrcIndexMask);
     std::ostringstream e;
-    e << ((src & kSrcRecovery) ? "B1" : "B0") << " + " << (src & kSrcIndexMask) << "ull * sb + off";
+    if (src & kSrcXorScratch)
+      e << "ldx(B1 + " << idx << "ull * sb + off, B2 + " << idx << "ull * sb + off)";
+    else
+      e << "ld(" << ((src & kSrcRecovery) ? "B1" : "B0") << " + " << idx << "ull * sb + off)";
     return e.str();
   };
   for (uint32_t tile = 0; tile < n_tiles; tile++) {
@@ -262,7 +287,7 @@ std::string generate(const NetSpec &spec, const std::string &name) {
     const uint32_t ahead = static_cast<uint32_t>(tu.prefetch);
     for (uint32_t t = 0; t < n_in; t++) {
       for (uint32_t u = t ? t + ahead : 0; u <= t + ahead && u < n_in; u++)
-        o << "  const Raw R" << u << " = ld(" << in_expr(u) << ");\n";
+        o << "  const Raw R" << u << " = " << load_expr(u) << ";\n";
       o << "  {\n";
       o << "  u32 P[16];\n  planes(R" << t << ", P);\n";
       std::vector<uint16_t> rows(n_acc, 0);
@@ -294,7 +319,10 @@ std::string generate(const NetSpec &spec, const std::string &name) {
 namespace {
 
 std::mutex g_mu;
+std::condition_variable g_cv;                              // signalled when a background compile ends
 std::map<std::string, std::unique_ptr<Kernel>> g_cache;  // key: device + spec bytes
+std::map<std::string, std::string> g_failed;              // key -> compile error (background compiles)
+std::set<std::string> g_pending;                          // keys compiling in the background
 
 std::string spec_key(const NetSpec &s, int dev) {
   std::string k = std::to_string(dev) + ":" + s.role + ":" + tuning_key(tuning()) + ":" + std::to_string(s.n_in) + ":" +
@@ -324,6 +352,7 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &err) 
     err = "hiprtcCreateProgram failed";
     return false;
   }
+  // -O1/-O2 measured no faster to compile (the time is in the backend)
   const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
   if (rc != HIPRTC_SUCCESS) {
@@ -366,17 +395,10 @@ bool enabled() {
   return !(e && std::strcmp(e, "0") == 0);
 }
 
-const Kernel *get(const NetSpec &spec, std::string &err) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    err = "hipGetDevice failed";
-    return nullptr;
-  }
-  const std::string key = spec_key(spec, dev);
-  std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_cache.find(key);
-  if (it != g_cache.end()) return it->second.get();
+namespace {
 
+// source -> loaded module; no lock held (compiles run concurrently)
+std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, std::string &err) {
   const std::string name = kernel_name(spec, key);
   const std::string src = generate(spec, name);
   const auto t0 = std::chrono::steady_clock::now();
@@ -402,13 +424,139 @@ const Kernel *get(const NetSpec &spec, std::string &err) {
   if (std::getenv("RS_AMD_JIT_VERBOSE"))
     std::fprintf(stderr, "[rs_amd jit] %s compiled in %.0f ms (%zu B source, %zu B code)\n", name.c_str(),
                  k->compile_ms, src.size(), code.size());
+  return k;
+}
+
+const Kernel *insert(const std::string &key, std::unique_ptr<Kernel> k) {  // g_mu held
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) return it->second.get();  // another thread won the race
   const Kernel *out = k.get();
   g_cache.emplace(key, std::move(k));
   return out;
 }
 
+// One background worker compiles the queued maps in order. At unload it drops the
+// queue and finishes only the compile in flight; it is defined after the caches
+// above, so it is destroyed (joined) before them.
+struct Job {
+  NetSpec spec;
+  std::string key;
+  int dev;
+};
+
+struct Worker {
+  std::thread th;
+  std::deque<Job> queue;
+  std::condition_variable wake;
+  bool stop = false;
+
+  void push(Job j) {  // g_mu held
+    queue.push_back(std::move(j));
+    if (!th.joinable()) th = std::thread([this] { run(); });
+    wake.notify_one();
+  }
+  void run() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(g_mu);
+        wake.wait(lk, [this] { return stop || !queue.empty(); });
+        if (stop) return;
+        j = std::move(queue.front());
+        queue.pop_front();
+      }
+      std::string e;
+      std::unique_ptr<Kernel> k;
+      if (hipSetDevice(j.dev) == hipSuccess) k = build(j.spec, j.key, e);
+      else e = "hipSetDevice failed";
+      std::lock_guard<std::mutex> lk(g_mu);
+      if (k) insert(j.key, std::move(k));
+      else g_failed.emplace(j.key, e);
+      g_pending.erase(j.key);
+      g_cv.notify_all();
+    }
+  }
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      stop = true;
+      for (const Job &j : queue) g_pending.erase(j.key);
+      queue.clear();
+      g_cv.notify_all();
+    }
+    wake.notify_all();
+    if (th.joinable()) th.join();
+  }
+} g_worker;
+
+bool env_on(const char *name) {
+  const char *e = std::getenv(name);
+  return e && *e && std::strcmp(e, "0") != 0;
+}
+
+}  // namespace
+
+uint64_t max_async_blocks() {
+  const int v = env_int("RS_AMD_NET_ASYNC_BLOCKS", -1);
+  return v >= 0 ? static_cast<uint64_t>(v) : kMaxAsyncBlocks;
+}
+
+bool supports_async(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
+  const uint64_t blocks = static_cast<uint64_t>(n_in) * ((n_out + kTileOut - 1) / kTileOut);
+  return n_in > 0 && n_out > 0 && n_out <= kMaxOut && blocks <= std::max(max_blocks(), max_async_blocks()) &&
+         shard_bytes % kUnitBytes == 0 && shard_bytes < (1ull << 32);
+}
+
+const Kernel *get(const NetSpec &spec, std::string &err) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    err = "hipGetDevice failed";
+    return nullptr;
+  }
+  const std::string key = spec_key(spec, dev);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(key);
+    if (it != g_cache.end()) return it->second.get();
+  }
+  std::unique_ptr<Kernel> k = build(spec, key, err);
+  if (!k) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  return insert(key, std::move(k));
+}
+
+const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
+  pending = false;
+  if (env_on("RS_AMD_JIT_SYNC")) return get(spec, err);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    err = "hipGetDevice failed";
+    return nullptr;
+  }
+  const std::string key = spec_key(spec, dev);
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) return it->second.get();
+  auto f = g_failed.find(key);
+  if (f != g_failed.end()) {
+    err = f->second;
+    return nullptr;
+  }
+  pending = true;
+  if (g_pending.count(key)) return nullptr;
+  g_pending.insert(key);
+  g_worker.push(Job{spec, key, dev});
+  return nullptr;
+}
+
+void wait_pending() {
+  std::unique_lock<std::mutex> lk(g_mu);
+  g_cv.wait(lk, [] { return g_pending.empty(); });
+}
+
 hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const uint8_t *buf1, uint64_t stride1,
-                  uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s) {
+                  uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s,
+                  const uint8_t *buf2, uint64_t stride2) {
   const uint64_t units = shard_bytes / kUnitBytes;
   const uint64_t per_block = 4ull * k.units;
   // unit groups padded to a multiple of 8 (one per XCD, see generate()); the padding
@@ -419,8 +567,10 @@ hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const 
     const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
     const unsigned char *a0 = buf0, *a1 = buf1 ? buf1 : buf0;
     unsigned char *o = out;
+    const unsigned char *a2 = buf2 ? buf2 : a1;
     uint64_t st0 = stride0, st1 = buf1 ? stride1 : stride0, so = out_stride, sb = shard_bytes, first = s0;
-    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sb, &first};
+    uint64_t st2 = buf2 ? stride2 : st1;
+    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sb, &first, &a2, &st2};
     hipError_t e = hipModuleLaunchKernel(k.fn, gx, gy, 1, 256, 1, 1, 0, s, args, nullptr);
     if (e != hipSuccess) return e;
   }

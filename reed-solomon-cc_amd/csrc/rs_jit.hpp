@@ -39,7 +39,16 @@ constexpr uint32_t kTileOut = 4;      // outputs per wave (64 accumulator planes
 constexpr uint32_t kMaxOut = 64;      // tiles of kTileOut, one workgroup each
 // generated code size: n_in x tiles input blocks of ~270 instructions each; hipRTC
 // takes ~20-40 ms per block, so the cap keeps a plan's compile near 1-2 s
+// (RS_AMD_NET_MAX_BLOCKS overrides it, see max_blocks())
 constexpr uint64_t kMaxBlocks = 64;
+uint64_t max_blocks();
+// Larger maps (the e x e syndrome map of wide codes: RS(200,55) losing 55 is 770
+// blocks, ~16-36 s) compile in a background thread while the plan's table kernel
+// runs; RS_AMD_NET_ASYNC_BLOCKS overrides the cap (0 = never), RS_AMD_JIT_SYNC=1
+// compiles them in the calling thread instead.
+constexpr uint64_t kMaxAsyncBlocks = 1024;
+uint64_t max_async_blocks();
+bool supports_async(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
 
 bool enabled();  // RS_AMD_JIT != 0 and hipRTC usable
 bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
@@ -59,12 +68,22 @@ struct Kernel {
 // nullptr and sets `err` when hipRTC is unavailable or compilation fails.
 const Kernel *get(const NetSpec &spec, std::string &err);
 
+// Same, for maps past the synchronous cap: returns the kernel once compiled; until
+// then nullptr with pending = true (a background compile has been started), or
+// nullptr with pending = false and `err` set if the compile failed.
+const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending);
+
+// Block until no background compile is running (rs_net_wait).
+void wait_pending();
+
 // Generate and compile `spec` with hipRTC only (no device needed): a build check.
 bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *code_bytes);
 
-// buf0/buf1: input buffers ([stripe][shard][sb]); out: [stripe][n_out][sb].
+// buf0/buf1: input buffers ([stripe][shard][sb]); out: [stripe][n_out][sb]. An input
+// flagged kSrcXorScratch is buf1[idx] ^ buf2[idx] (buf2: [stripe][..][sb], stride2).
 hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const uint8_t *buf1, uint64_t stride1,
-                  uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s);
+                  uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s,
+                  const uint8_t *buf2 = nullptr, uint64_t stride2 = 0);
 
 }  // namespace jit
 }  // namespace rs

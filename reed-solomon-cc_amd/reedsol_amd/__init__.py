@@ -84,6 +84,7 @@ def lib():
         "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
         "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
         "rs_net_compile_check": (C.c_int, [u64, u64, vp, u32, vp]),
+        "rs_net_wait": (C.c_int, []),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_mul_scalar": (C.c_int, [vp, sz, C.c_uint16, u32]),
@@ -310,6 +311,11 @@ def net_compile_check(k, m, present=None, flags=0) -> float:
     pres = None if present is None else (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
     _check(lib().rs_net_compile_check(k, m, pres, flags, C.byref(ms)))
     return ms.value
+
+
+def net_wait() -> None:
+    """Block until no background network compile is running (include/reedsol.h)."""
+    _check(lib().rs_net_wait())
 
 
 # ------------------------------------------------------------ engine test shims

@@ -122,6 +122,14 @@ def test_kernel_selection_network():
     assert R.reconstruct_kernel_name(16, 4, 8192, present) == "net_reconstruct_i16_o1"
     assert R.encode_kernel_name(10, 4, 2048) == "encode_reg_w4_nv4"  # not a whole 4 KiB unit
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"  # more than 16 outputs
+    # wide code, 55 erasures: the 55 x 55 syndrome map is a (background-compiled) network
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+net_syndrome_i55_o55"
+
+
+def test_kernel_selection_async_cap(monkeypatch):
+    """RS_AMD_NET_ASYNC_BLOCKS=0 keeps large maps on the table kernels."""
+    monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+decode_mtile16_nv1"
 
 
 def test_kernel_selection(monkeypatch):
@@ -151,3 +159,8 @@ def test_net_kernels_compile_for_gfx950():
     assert R.net_compile_check(4, 2, None, 3) > 0
     with pytest.raises(R.InvalidArgument):
         R.net_compile_check(200, 55)  # 55 outputs: no network form
+    # 8 of 200 data shards lost: syndrome map 8 x 8 (16 input blocks)
+    present = [1] * 255
+    for i in range(0, 16, 2):
+        present[i] = 0
+    assert R.net_compile_check(200, 55, present) > 0

@@ -87,3 +87,23 @@ def test_syndrome_rs200_55_full_size_all_erasures():
     assert R.reconstruct_kernel_name(k, m, sb, present).startswith("syndrome")
     got = reconstruct(k, m, present, data, par.cpu().numpy())
     assert (got == data[:, erase]).all()
+
+
+def test_syndrome_network_background_compile(oracle, monkeypatch):
+    """RS(200,55) losing 55 data shards: the 55 x 55 syndrome map (770 network blocks)
+    compiles in the background; the calls before it is ready run the table kernel,
+    the calls after it the network — both restore the erased shards bit-exactly."""
+    monkeypatch.delenv("RS_AMD_JIT", raising=False)
+    monkeypatch.delenv("RS_AMD_JIT_SYNC", raising=False)
+    k, m, sb, n = 200, 55, 8192, 2
+    rng = np.random.default_rng(2055)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data)
+    lost = sorted(int(i) for i in rng.choice(k, size=55, replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    assert R.reconstruct_kernel_name(k, m, sb, present) == "syndrome+encode_ws64_nv1+net_syndrome_i55_o55"
+    for _ in range(2):  # 2nd use queues the compile (RS_AMD_NET_ASYNC_AFTER)
+        assert (reconstruct(k, m, present, data, par) == data[:, lost]).all()
+    R.net_wait()
+    assert (reconstruct(k, m, present, data, par) == data[:, lost]).all()
