@@ -1515,10 +1515,12 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
     const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
     const char *ev = getenv("RS_AMD_WS64_SHARED");  // A/B switch: 1 (default) shared stage tables
     const bool shared = !(ev && ev[0] == '0');
-    // A/B switch, default off: LDS-staged VGPR tables measured 10.2 vs 9.3 ms (NV=1,
-    // occupancy 5 -> 3 waves/SIMD at 151 VGPRs) and 10.0 vs 10.7 ms (NV=2) on RS(200,55)
+    // A/B switch RS_AMD_WS64_LDS, default on: LDS-staged VGPR tables (no SGPR->VGPR
+    // moves, no SGPR spills). RS(200,55) 256 KiB x 256 after the load split: NV=1 7.36
+    // vs 7.62 ms, NV=2 9.34 vs 11.5 ms (profiles/r01/sweep_rs200_55_ws64_lds.jsonl;
+    // before the split, when every load was its own round trip, it measured slower)
     const char *el = getenv("RS_AMD_WS64_LDS");
-    if (el && el[0] == '1') {
+    if (!(el && el[0] == '0')) {
       if (kc.nv == 1) hipLaunchKernelGGL((k_encode_ws64l<1>), g, dim3(kBlock), 0, s, a);
       else hipLaunchKernelGGL((k_encode_ws64l<2>), g, dim3(kBlock), 0, s, a);
     } else {
