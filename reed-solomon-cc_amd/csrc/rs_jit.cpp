@@ -192,12 +192,16 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //   RS_AMD_NET_NT        non-temporal loads (bit 0) / stores (bit 1), default 3 for
 //                        one output tile, 2 for several (their inputs are re-read)
 //   RS_AMD_NET_UNITS     4 KiB units per wave, walked in a loop (default 1)
+//   RS_AMD_NET_TILE      outputs per workgroup, 4 (64 accumulator planes) or 8 (default:
+//                        half the input re-reads and plane transforms of multi-tile maps;
+//                        RS(32,8) encode 2.39 -> 1.91 ms, the 55 x 55 syndrome map
+//                        13.9 -> 12.3 ms reconstruct, profiles/r01/sweep_net_tile8.jsonl)
 //   RS_AMD_NET_BARRIER   sched_barrier between inputs: bounds the scheduling regions,
 //                        so compile time stays ~linear in size (1 on, 0 off, default
 //                        -1: on above 16 input blocks; off costs nothing to compile
 //                        for small networks and measured ~1.5% faster on RS(10,4))
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8;
 };
 
 int env_int(const char *name, int def) {
@@ -212,12 +216,13 @@ Tuning tuning() {
   t.nt = env_int("RS_AMD_NET_NT", t.nt) & 3;
   t.barrier = env_int("RS_AMD_NET_BARRIER", t.barrier);
   t.units = std::max(1, std::min(64, env_int("RS_AMD_NET_UNITS", t.units)));
+  t.tile = env_int("RS_AMD_NET_TILE", t.tile) >= 8 ? 8 : 4;
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
   return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt) + "b" +
-         std::to_string(t.barrier) + "u" + std::to_string(t.units);
+         std::to_string(t.barrier) + "u" + std::to_string(t.units) + "t" + std::to_string(t.tile);
 }
 
 }  // namespace
@@ -235,8 +240,9 @@ bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
 
 std::string generate(const NetSpec &spec, const std::string &name) {
   const uint32_t n_in = spec.n_in, n_out = spec.n_out;
-  const uint32_t n_tiles = (n_out + kTileOut - 1) / kTileOut;
   const Tuning tu = tuning();
+  const uint32_t tw = static_cast<uint32_t>(tu.tile);  // outputs per workgroup
+  const uint32_t n_tiles = (n_out + tw - 1) / tw;
   std::ostringstream o;
   // several output tiles re-read every input through L2: non-temporal loads (which
   // evict early) cost 10-15 % there, so by default they are kept for 1-tile maps only
@@ -277,7 +283,7 @@ std::string generate(const NetSpec &spec, const std::string &name) {
     return e.str();
   };
   for (uint32_t tile = 0; tile < n_tiles; tile++) {
-    const uint32_t j0 = tile * kTileOut, nj = std::min(kTileOut, n_out - j0);
+    const uint32_t j0 = tile * tw, nj = std::min(tw, n_out - j0);
     const size_t n_acc = 16 * nj;
     o << "  " << (tile ? "else if" : "if") << " (tile == " << tile << "u) {\n";
     o << "  u32 ";
@@ -417,7 +423,7 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, std::
   }
   k->n_in = spec.n_in;
   k->n_out = spec.n_out;
-  k->n_tiles = (spec.n_out + kTileOut - 1) / kTileOut;
+  k->n_tiles = (spec.n_out + tuning().tile - 1) / tuning().tile;
   k->units = static_cast<uint32_t>(tuning().units);
   k->name = name;
   k->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

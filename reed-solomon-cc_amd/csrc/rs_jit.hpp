@@ -35,8 +35,8 @@ struct NetSpec {
 // Lanes cover 4 KiB of every shard per wave (32 symbols per lane): shard_bytes
 // must be a multiple of this, and below 4 GiB (32-bit lane offsets).
 constexpr uint64_t kUnitBytes = 4096;
-constexpr uint32_t kTileOut = 4;      // outputs per wave (64 accumulator planes)
-constexpr uint32_t kMaxOut = 64;      // tiles of kTileOut, one workgroup each
+constexpr uint32_t kTileOut = 4;      // size caps count blocks of one input x 4 outputs
+constexpr uint32_t kMaxOut = 64;      // tiles of 8 outputs (RS_AMD_NET_TILE), one workgroup each
 // generated code size: n_in x tiles input blocks of ~270 instructions each; hipRTC
 // takes ~20-40 ms per block, so the cap keeps a plan's compile near 1-2 s
 // (RS_AMD_NET_MAX_BLOCKS overrides it, see max_blocks())
