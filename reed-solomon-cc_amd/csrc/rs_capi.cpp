@@ -261,8 +261,9 @@ bool encode_net_async(uint64_t k, uint64_t m, uint64_t sb, int max_nv) {
 
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out) {
   char key[128];
-  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu", dev, (unsigned long long)k, (unsigned long long)m, flags,
-                static_cast<unsigned long long>(jit::max_blocks()));
+  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu/%llu", dev, (unsigned long long)k, (unsigned long long)m,
+                flags, static_cast<unsigned long long>(jit::max_blocks()),
+                static_cast<unsigned long long>(jit::max_async_blocks()));
   std::lock_guard<std::mutex> lk(g_plan_mu);
   auto it = g_enc_plans.find(key);
   if (it != g_enc_plans.end()) {
@@ -367,6 +368,13 @@ uint64_t fft_encode_mul_count(uint64_t k, uint64_t m) {
   return n;
 }
 
+bool direct_net_async(uint64_t k, uint64_t e, uint64_t n_in, uint64_t sb, const std::string &mode) {
+  (void)k;
+  return (mode == "auto" || mode == "net") && jit::enabled() &&
+         !jit::supports(static_cast<uint32_t>(n_in), static_cast<uint32_t>(e), sb) &&
+         jit::supports_async(static_cast<uint32_t>(n_in), static_cast<uint32_t>(e), sb);
+}
+
 // Reconstruct by syndromes instead of the k x e matrix: worth it for wide codes
 // with many erasures (RS(200,55) losing 55: 785 + 0.75*55^2 multiplies per column
 // against 0.75*200*55). Needs the corrected multiply (under D1 the literal
@@ -444,7 +452,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
                     std::to_string(jit::enabled() && sb % jit::kUnitBytes == 0 && sb < (1ull << 32)) + "/" +
-                    std::to_string(jit::max_blocks()) + "/";
+                    std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::lock_guard<std::mutex> lk(g_plan_mu);
@@ -465,7 +473,10 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   const bool use_net = (mode == "auto" || mode == "net") && jit::enabled() &&
                        jit::supports(static_cast<uint32_t>(n_in_want), static_cast<uint32_t>(e), sb);
   if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
-  const bool use_syn = !use_net && syndrome_pick(k, m, e, flags, sb, mode);
+  // past the synchronous cap: the same map compiled in the background, the matrix
+  // kernel meanwhile (RS(200,55) losing 8: 400 blocks, against syndrome + encode)
+  const bool use_net_async = !use_net && kind != 0 && direct_net_async(k, e, n_in_want, sb, mode);
+  const bool use_syn = !use_net && !use_net_async && syndrome_pick(k, m, e, flags, sb, mode);
   if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
   // the syndromes' e x e map as a network too (its table kernel stays the fallback)
   const bool syn_net = use_syn && (mode == "auto" || mode == "net" || mode == "syndrome") && jit::enabled() &&
@@ -505,7 +516,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     if (st) return st;
     plan->matrix = true;
     plan->tiled = kind == 2;
-    if (use_net || syn_net) {
+    if (use_net || use_net_async || syn_net) {
       plan->net = std::make_shared<NetSlot>();
       plan->net->async = !jit::supports(map.n_in, map.n_out, sb);
       plan->net->spec = std::move(map);
@@ -914,6 +925,8 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
     return net_name("reconstruct", k, e);
+  if (decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(k, e, k, sb, mode))
+    return net_name("reconstruct", k, e);
   if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
     thread_local std::string name;
     name = std::string("syndrome+") + choose_encode(k, m, sb, 4).name + "+";
@@ -948,7 +961,7 @@ int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_
     for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
     if (is_low_rate(k, m)) {
       if ((st = low_decode_map(k, m, flags, present, spec))) return st;
-    } else if (!jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), jit::kUnitBytes) &&
+    } else if (!jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(e), jit::kUnitBytes) &&
                syndrome_pick(k, m, e, flags, jit::kUnitBytes * 64, "auto")) {
       if ((st = syndrome_map(k, m, present, spec))) return st;  // the plan's e x e map
     } else {
@@ -959,8 +972,7 @@ int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_
   } else {
     encode_map(k, m, flags, spec);
   }
-  if (!(spec.role == "syndrome" ? jit::supports_async(spec.n_in, spec.n_out, jit::kUnitBytes)
-                                 : jit::supports(spec.n_in, spec.n_out, jit::kUnitBytes)))
+  if (!jit::supports_async(spec.n_in, spec.n_out, jit::kUnitBytes))  // also the background-compiled sizes
     return fail(RS_ERR_INVALID_ARGUMENT, "no network form");
   std::string err;
   if (!jit::compile_check(spec, err, compile_ms, nullptr)) return fail(RS_ERR_DEVICE, err);

@@ -162,8 +162,9 @@ def test_net_kernels_compile_for_gfx950():
     assert R.net_compile_check(4, 2, None, 3) > 0
     with pytest.raises(R.InvalidArgument):
         R.net_compile_check(200, 55)  # 55 outputs: no network form
-    # 8 of 200 data shards lost: syndrome map 8 x 8 (16 input blocks)
+    # 32 of 200 data shards lost: the direct map (1,600 blocks) is past the background
+    # cap, so the plan's network is the 32 x 32 syndrome map (256 blocks)
     present = [1] * 255
-    for i in range(0, 16, 2):
+    for i in range(0, 64, 2):
         present[i] = 0
     assert R.net_compile_check(200, 55, present) > 0
