@@ -690,6 +690,7 @@ int build_map_plan(int dev, jit::NetSpec &&spec, std::shared_ptr<MapPlan> &out) 
   int st = upload(blob.data(), blob.size(), dev, p->buf);
   if (st) return st;
   p->net = std::make_shared<NetSlot>();
+  p->net->async = !jit::supports(p->n_in, p->n_out, jit::kUnitBytes);  // larger maps: background compile
   p->net->spec = std::move(spec);
   out = p;
   return RS_OK;
@@ -700,7 +701,7 @@ int run_map(const MapPlan &p, uint64_t sb, uint64_t n, const uint8_t *b0, uint64
             uint8_t *out, uint64_t so, int max_nv, hipStream_t s) {
   if (!b0) b0 = b1;
   if (!b1) b1 = b0;
-  if (max_nv == 4 && jit::enabled() && jit::supports(p.n_in, p.n_out, sb))
+  if (max_nv == 4 && jit::enabled() && jit::supports_async(p.n_in, p.n_out, sb))
     if (const jit::Kernel *nk = net_kernel(*p.net)) {
       HIP_TRY(jit::launch(*nk, b0, s0, b1, s1, out, so, sb, n, s));
       return RS_OK;
@@ -898,7 +899,7 @@ static const char *net_name(const char *role, uint64_t n_in, uint64_t n_out) {
 
 const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
   if (is_low_rate(k, m)) {
-    if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))
+    if (jit::enabled() && jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))
       return net_name("encode_low", k, m);
     return "lowrate_matrix";
   }
@@ -917,7 +918,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
   if (is_low_rate(k, m)) {
-    if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
+    if (jit::enabled() && jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
       return net_name("reconstruct_low", k, e);
     return "lowrate_matrix";
   }

@@ -71,10 +71,13 @@ def test_low_rate_network_compiles(k, m):
     assert R.net_compile_check(k, m) > 0
 
 
-def test_low_rate_limits():
+def test_low_rate_limits(monkeypatch):
     with pytest.raises(R.LowRateUnsupported):
         R.Encoder(2, 100, 64)
     assert R.encode_kernel_name(10, 20, 1 << 16) == "net_encode_low_i10_o20"
+    # 256 blocks: a background-compiled network (table matrix kernel until it is ready)
+    assert R.encode_kernel_name(16, 64, 1 << 16) == "net_encode_low_i16_o64"
+    monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
     assert R.encode_kernel_name(16, 64, 1 << 16) == "lowrate_matrix"
 
 
@@ -135,3 +138,29 @@ def test_low_rate_exhaustive_rs3_5_one_shot():
             with pytest.raises(R.NotEnoughShards):
                 R.decode(k, m, o, r)
     assert ok == sum(1 for mask in range(1 << 8) if bin(mask).count("1") <= 5)
+
+
+@pytest.mark.gpu
+@gpu
+def test_low_rate_background_network(oracle, monkeypatch):
+    """RS(16,64) low rate: the 16 x 64 encode map (256 blocks) compiles in the
+    background; table-kernel calls before, network calls after, all == oracle."""
+    monkeypatch.delenv("RS_AMD_JIT", raising=False)
+    monkeypatch.delenv("RS_AMD_JIT_SYNC", raising=False)
+    k, m, sb, n = 16, 64, 8192, 2
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(1664)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = np.stack([oracle.encode_low(k, m, data[s])[1] for s in range(n)])
+    d = torch.from_numpy(data).to(dev)
+
+    def enc():
+        p = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
+        R.encode_batch_dev(k, m, d, p)
+        torch.cuda.synchronize()
+        return p.cpu().numpy()
+
+    for _ in range(2):
+        assert (enc() == exp).all()
+    R.net_wait()
+    assert (enc() == exp).all()
