@@ -1444,36 +1444,55 @@ hipError_t copy_rows(void *dst, uint64_t dst_stride, const void *src, uint64_t s
   return hipMemcpy2DAsync(dst, dst_stride, src, src_stride, row_bytes, rows, kind, s);
 }
 
-// Per-device staging ring of the host-batch calls: kSlots slices, each on its own
+// Per-device staging ring of the host-batch calls: `slots` slices, each on its own
 // stream (H2D -> kernel -> D2H in order; slices on different streams overlap both
 // PCIe directions with the kernels). Buffers and streams persist across calls and
 // grow on demand; the ring's mutex serialises host-batch calls on one device.
 struct Pipeline {
-  static constexpr int kSlots = 3;
+  static constexpr int kMaxSlots = 8;
   std::mutex mu;
-  hipStream_t st[kSlots] = {};
-  void *buf[kSlots][3] = {};
+  int slots = 0;  // ring depth in use (RS_AMD_HOST_SLOTS, default 3)
+  hipStream_t st[kMaxSlots] = {};
+  void *buf[kMaxSlots][3] = {};
   uint64_t cap[3] = {};
-  int ensure(const uint64_t bytes[3]) {
-    for (int i = 0; i < kSlots; i++)
+  int ensure(const uint64_t bytes[3], int want) {
+    for (int i = 0; i < want; i++)
       if (!st[i]) HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-    for (int j = 0; j < 3; j++) {
-      if (bytes[j] <= cap[j]) continue;
-      for (int i = 0; i < kSlots; i++) {
+    bool grow = want != slots;
+    for (int j = 0; j < 3; j++) grow = grow || bytes[j] > cap[j];
+    if (!grow) return RS_OK;
+    for (int i = 0; i < kMaxSlots; i++)
+      for (int j = 0; j < 3; j++) {
         if (buf[i][j]) HIP_TRY(hipFree(buf[i][j]));
         buf[i][j] = nullptr;
       }
-      cap[j] = 0;
-      for (int i = 0; i < kSlots; i++) HIP_TRY(hipMalloc(&buf[i][j], bytes[j]));
-      cap[j] = bytes[j];
-    }
+    slots = 0;
+    for (int j = 0; j < 3; j++) cap[j] = std::max(cap[j], bytes[j]);
+    for (int i = 0; i < want; i++)
+      for (int j = 0; j < 3; j++)
+        if (cap[j]) HIP_TRY(hipMalloc(&buf[i][j], cap[j]));
+    slots = want;
     return RS_OK;
   }
   int finish() {
-    for (int i = 0; i < kSlots; i++) HIP_TRY(hipStreamSynchronize(st[i]));
+    for (int i = 0; i < slots; i++) HIP_TRY(hipStreamSynchronize(st[i]));
     return RS_OK;
   }
 };
+
+// ring shape (env, read per call): RS_AMD_HOST_SLOTS (1..8, default 2) slices of
+// RS_AMD_HOST_SLICE_MB input MiB (default 256). Pinned RS(10,4) 1 MiB x 512 encode /
+// reconstruct GiB/s: 1 slot 37.5 / 37.0, 2 slots 49.3 / 49.8, 3 slots 44.6 / 48.8,
+// 6 x 64 MiB 46.4 / 46.2 (profiles/r01/e2e_shapes): two slices keep one H2D, one
+// kernel and one D2H in flight; more streams only contend for the copy engines.
+int host_slots() {
+  const char *e = std::getenv("RS_AMD_HOST_SLOTS");
+  return e && *e ? std::max(1, std::min(Pipeline::kMaxSlots, std::atoi(e))) : 2;
+}
+uint64_t host_slice_bytes() {
+  const char *e = std::getenv("RS_AMD_HOST_SLICE_MB");
+  return (e && *e ? static_cast<uint64_t>(std::max(1, std::atoi(e))) : 256ull) << 20;
+}
 
 // process-lifetime rings (never freed: the HIP runtime reclaims them at exit)
 std::mutex g_pipe_mu;
@@ -1488,7 +1507,6 @@ struct Pipelines {
   }
 };
 
-constexpr uint64_t kSliceBytes = 256ull << 20;  // input bytes per pipeline slice
 
 }  // namespace
 
@@ -1503,13 +1521,14 @@ int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const vo
   if (rec_stride == 0) rec_stride = m * sb;
   int dev;
   if ((st = current_device(&dev))) return st;
-  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, kSliceBytes / (k * sb)));
+  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
+  const int slots = host_slots();
   Pipeline &p = Pipelines::of(dev);
   std::lock_guard<std::mutex> lk(p.mu);
   const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
-  if ((st = p.ensure(bytes))) return st;
+  if ((st = p.ensure(bytes, slots))) return st;
   for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
-    const int slot = static_cast<int>(i % Pipeline::kSlots);
+    const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
     const uint64_t cnt = std::min(S, n - s0);
     hipStream_t q = p.st[slot];
     HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride, orig_stride,
@@ -1538,13 +1557,14 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
   if (out_stride == 0) out_stride = e * sb;
   int dev;
   if ((st = current_device(&dev))) return st;
-  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, kSliceBytes / (k * sb)));
+  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
+  const int slots = host_slots();
   Pipeline &p = Pipelines::of(dev);
   std::lock_guard<std::mutex> lk(p.mu);
   const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
-  if ((st = p.ensure(bytes))) return st;
+  if ((st = p.ensure(bytes, slots))) return st;
   for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
-    const int slot = static_cast<int>(i % Pipeline::kSlots);
+    const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
     const uint64_t cnt = std::min(S, n - s0);
     hipStream_t q = p.st[slot];
     // only the present shards cross PCIe
