@@ -442,3 +442,26 @@ def test_more_than_65535_stripes(oracle):
     idx = [0, 65533, 65534, 65535, 65536, n - 1]
     sample = d[idx].cpu().numpy()
     assert (p[idx].cpu().numpy() == oracle.encode_batch(k, m, sample)).all()
+
+
+@pytest.mark.parametrize("k,m", [(16, 16), (32, 8), (12, 12)])
+def test_net_tile_widths_agree(oracle, monkeypatch, k, m):
+    """8-output (default) and 4-output network tiles, encode and reconstruct of
+    multi-tile maps: identical bytes, equal to the oracle."""
+    rng = np.random.default_rng(k * 31 + m)
+    sb, n = 8192, 2
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = oracle.encode_batch(k, m, data)
+    lost = sorted(int(i) for i in rng.choice(k, size=min(k, m), replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    for tile in ("8", "4"):
+        monkeypatch.setenv("RS_AMD_NET_TILE", tile)
+        d = to_dev(data)
+        p = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+        R.encode_batch_dev(k, m, d, p)
+        out = torch.zeros((n, len(lost), sb), dtype=torch.uint8, device=DEV)
+        R.reconstruct_batch_dev(k, m, present, d, p, out)
+        torch.cuda.synchronize()
+        assert (p.cpu().numpy() == exp).all(), tile
+        assert (out.cpu().numpy() == data[:, lost]).all(), tile
