@@ -238,9 +238,17 @@ bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
          shard_bytes < (1ull << 32);
 }
 
-std::string generate(const NetSpec &spec, const std::string &name) {
+namespace {
+std::string generate_with(const NetSpec &spec, const std::string &name, const Tuning &tu);
+}
+
+std::string generate(const NetSpec &spec, const std::string &name) { return generate_with(spec, name, tuning()); }
+
+namespace {
+// the knobs are captured when a compile is requested (a background job must not see
+// the environment of a later moment: the cache key already names these values)
+std::string generate_with(const NetSpec &spec, const std::string &name, const Tuning &tu) {
   const uint32_t n_in = spec.n_in, n_out = spec.n_out;
-  const Tuning tu = tuning();
   const uint32_t tw = static_cast<uint32_t>(tu.tile);  // outputs per workgroup
   const uint32_t n_tiles = (n_out + tw - 1) / tw;
   std::ostringstream o;
@@ -320,6 +328,7 @@ std::string generate(const NetSpec &spec, const std::string &name) {
   o << "  }\n}\n";  // unit loop, kernel
   return o.str();
 }
+}  // namespace
 
 // ------------------------------------------------------------- compile + cache
 namespace {
@@ -330,8 +339,8 @@ std::map<std::string, std::unique_ptr<Kernel>> g_cache;  // key: device + spec b
 std::map<std::string, std::string> g_failed;              // key -> compile error (background compiles)
 std::set<std::string> g_pending;                          // keys compiling in the background
 
-std::string spec_key(const NetSpec &s, int dev) {
-  std::string k = std::to_string(dev) + ":" + s.role + ":" + tuning_key(tuning()) + ":" + std::to_string(s.n_in) + ":" +
+std::string spec_key(const NetSpec &s, int dev, const Tuning &tu) {
+  std::string k = std::to_string(dev) + ":" + s.role + ":" + tuning_key(tu) + ":" + std::to_string(s.n_in) + ":" +
                   std::to_string(s.n_out) + ":";
   k.append(reinterpret_cast<const char *>(s.src.data()), s.src.size() * sizeof(int32_t));
   k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
@@ -383,7 +392,8 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &err) 
 bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *code_bytes) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
-  const std::string name = kernel_name(spec, spec_key(spec, -1)), src = generate(spec, name);
+  const Tuning tu = tuning();
+  const std::string name = kernel_name(spec, spec_key(spec, -1, tu)), src = generate_with(spec, name, tu);
   if (const char *dir = std::getenv("RS_AMD_JIT_DUMP")) {  // debug aid: keep the generated source
     if (FILE *f = std::fopen((std::string(dir) + "/" + name + ".hip").c_str(), "w")) {
       std::fputs(src.c_str(), f);
@@ -404,9 +414,9 @@ bool enabled() {
 namespace {
 
 // source -> loaded module; no lock held (compiles run concurrently)
-std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, std::string &err) {
+std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const Tuning &tu, std::string &err) {
   const std::string name = kernel_name(spec, key);
-  const std::string src = generate(spec, name);
+  const std::string src = generate_with(spec, name, tu);
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
   if (!compile(src, code, err)) return nullptr;
@@ -423,8 +433,8 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, std::
   }
   k->n_in = spec.n_in;
   k->n_out = spec.n_out;
-  k->n_tiles = (spec.n_out + tuning().tile - 1) / tuning().tile;
-  k->units = static_cast<uint32_t>(tuning().units);
+  k->n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
+  k->units = static_cast<uint32_t>(tu.units);
   k->name = name;
   k->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (std::getenv("RS_AMD_JIT_VERBOSE"))
@@ -448,6 +458,7 @@ struct Job {
   NetSpec spec;
   std::string key;
   int dev;
+  Tuning tu;
 };
 
 struct Worker {
@@ -473,7 +484,7 @@ struct Worker {
       }
       std::string e;
       std::unique_ptr<Kernel> k;
-      if (hipSetDevice(j.dev) == hipSuccess) k = build(j.spec, j.key, e);
+      if (hipSetDevice(j.dev) == hipSuccess) k = build(j.spec, j.key, j.tu, e);
       else e = "hipSetDevice failed";
       std::lock_guard<std::mutex> lk(g_mu);
       if (k) insert(j.key, std::move(k));
@@ -519,13 +530,14 @@ const Kernel *get(const NetSpec &spec, std::string &err) {
     err = "hipGetDevice failed";
     return nullptr;
   }
-  const std::string key = spec_key(spec, dev);
+  const Tuning tu = tuning();
+  const std::string key = spec_key(spec, dev, tu);
   {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
     if (it != g_cache.end()) return it->second.get();
   }
-  std::unique_ptr<Kernel> k = build(spec, key, err);
+  std::unique_ptr<Kernel> k = build(spec, key, tu, err);
   if (!k) return nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
   return insert(key, std::move(k));
@@ -539,7 +551,8 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
     err = "hipGetDevice failed";
     return nullptr;
   }
-  const std::string key = spec_key(spec, dev);
+  const Tuning tu = tuning();
+  const std::string key = spec_key(spec, dev, tu);
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_cache.find(key);
   if (it != g_cache.end()) return it->second.get();
@@ -551,7 +564,7 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
   pending = true;
   if (g_pending.count(key)) return nullptr;
   g_pending.insert(key);
-  g_worker.push(Job{spec, key, dev});
+  g_worker.push(Job{spec, key, dev, tu});
   return nullptr;
 }
 
