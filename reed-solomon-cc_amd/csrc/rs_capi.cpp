@@ -13,6 +13,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -854,6 +856,21 @@ int reconstruct_tail(uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint
 }  // namespace
 
 // ===================================================================== ABI
+// No C++ exception may cross the C ABI: host allocation failures become
+// RS_ERR_OUT_OF_MEMORY, anything else RS_ERR_DEVICE with its message.
+template <class F>
+int guarded(F &&f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc &) {
+    return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception &ex) {
+    return fail(RS_ERR_DEVICE, ex.what());
+  } catch (...) {
+    return fail(RS_ERR_DEVICE, "unexpected exception");
+  }
+}
+
 extern "C" {
 
 const char *rs_version(void) { return "rs-amd 0.1.0 (gfx950)"; }
@@ -946,282 +963,290 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
 }
 
 int rs_net_wait(void) {
-  jit::wait_pending();
-  return RS_OK;
+  return guarded([&]() -> int {
+    jit::wait_pending();
+    return RS_OK;
+  });
 }
 
 int rs_net_compile_check(uint64_t k, uint64_t m, const uint8_t *present, uint32_t flags, double *compile_ms) {
-  int st = check_codec(k, m, jit::kUnitBytes);
-  if (st) return st;
-  jit::NetSpec spec;
-  if (present) {
-    uint64_t have = 0;
-    for (uint64_t i = 0; i < k + m; i++) have += present[i] != 0;
-    if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
-    uint64_t e = 0;
-    for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
-    if (is_low_rate(k, m)) {
-      if ((st = low_decode_map(k, m, flags, present, spec))) return st;
-    } else if (!jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(e), jit::kUnitBytes) &&
-               syndrome_pick(k, m, e, flags, jit::kUnitBytes * 64, "auto")) {
-      if ((st = syndrome_map(k, m, present, spec))) return st;  // the plan's e x e map
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, jit::kUnitBytes);
+    if (st) return st;
+    jit::NetSpec spec;
+    if (present) {
+      uint64_t have = 0;
+      for (uint64_t i = 0; i < k + m; i++) have += present[i] != 0;
+      if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+      uint64_t e = 0;
+      for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+      if (is_low_rate(k, m)) {
+        if ((st = low_decode_map(k, m, flags, present, spec))) return st;
+      } else if (!jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(e), jit::kUnitBytes) &&
+                 syndrome_pick(k, m, e, flags, jit::kUnitBytes * 64, "auto")) {
+        if ((st = syndrome_map(k, m, present, spec))) return st;  // the plan's e x e map
+      } else {
+        reconstruct_map(k, m, flags, present, spec);
+      }
+    } else if (is_low_rate(k, m)) {
+      encode_low_map(k, m, flags, spec);
     } else {
-      reconstruct_map(k, m, flags, present, spec);
+      encode_map(k, m, flags, spec);
     }
-  } else if (is_low_rate(k, m)) {
-    encode_low_map(k, m, flags, spec);
-  } else {
-    encode_map(k, m, flags, spec);
-  }
-  if (!jit::supports_async(spec.n_in, spec.n_out, jit::kUnitBytes))  // also the background-compiled sizes
-    return fail(RS_ERR_INVALID_ARGUMENT, "no network form");
-  std::string err;
-  if (!jit::compile_check(spec, err, compile_ms, nullptr)) return fail(RS_ERR_DEVICE, err);
-  return RS_OK;
+    if (!jit::supports_async(spec.n_in, spec.n_out, jit::kUnitBytes))  // also the background-compiled sizes
+      return fail(RS_ERR_INVALID_ARGUMENT, "no network form");
+    std::string err;
+    if (!jit::compile_check(spec, err, compile_ms, nullptr)) return fail(RS_ERR_DEVICE, err);
+    return RS_OK;
+  });
 }
 
 int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const void *d_original,
                         uint64_t orig_stride, void *d_recovery, uint64_t rec_stride, uint32_t flags,
                         rs_stream_t stream) {
-  if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
-  int st = check_codec(k, m, sb);
-  if (st) return st;
-  if (n_stripes == 0) return RS_OK;
-  if (!d_original || !d_recovery) return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
-  if (orig_stride == 0) orig_stride = k * sb;
-  if (rec_stride == 0) rec_stride = m * sb;
-  if (sb % 64) {
+  return guarded([&]() -> int {
+    if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    if (n_stripes == 0) return RS_OK;
+    if (!d_original || !d_recovery) return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    if (sb % 64) {
+      int dev;
+      if ((st = current_device(&dev))) return st;
+      return encode_tail(k, m, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride,
+                         static_cast<uint8_t *>(d_recovery), rec_stride, flags, static_cast<hipStream_t>(stream));
+    }
+    if (orig_stride < k * sb || rec_stride < m * sb) return fail(RS_ERR_INVALID_ARGUMENT, "stripe stride too small");
+    const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
+                                 orig_stride, rec_stride});
+    if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
     int dev;
     if ((st = current_device(&dev))) return st;
-    return encode_tail(k, m, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride,
-                       static_cast<uint8_t *>(d_recovery), rec_stride, flags, static_cast<hipStream_t>(stream));
-  }
-  if (orig_stride < k * sb || rec_stride < m * sb) return fail(RS_ERR_INVALID_ARGUMENT, "stripe stride too small");
-  const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
-                               orig_stride, rec_stride});
-  if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
-  int dev;
-  if ((st = current_device(&dev))) return st;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (is_low_rate(k, m)) {
-    std::shared_ptr<MapPlan> lp;
-    if ((st = get_low_encode_plan(dev, k, m, flags, lp))) return st;
-    return run_map(*lp, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
-                   static_cast<uint8_t *>(d_recovery), rec_stride, max_nv, s);
-  }
-  std::shared_ptr<EncodePlan> plan;
-  if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
-  if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
-      (plan->net->async ? encode_net_async(k, m, sb, max_nv)
-                        : jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))) {
-    if (const jit::Kernel *nk = net_kernel(*plan->net)) {
-      HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
-                          static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (is_low_rate(k, m)) {
+      std::shared_ptr<MapPlan> lp;
+      if ((st = get_low_encode_plan(dev, k, m, flags, lp))) return st;
+      return run_map(*lp, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
+                     static_cast<uint8_t *>(d_recovery), rec_stride, max_nv, s);
+    }
+    std::shared_ptr<EncodePlan> plan;
+    if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
+    if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
+        (plan->net->async ? encode_net_async(k, m, sb, max_nv)
+                          : jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))) {
+      if (const jit::Kernel *nk = net_kernel(*plan->net)) {
+        HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
+                            static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));
+        return RS_OK;
+      }
+    }
+    const KernelChoice kc = choose_encode(k, m, sb, max_nv);
+    EncodeArgs a{};
+    a.data = static_cast<const uint8_t *>(d_original);
+    a.data_stripe_stride = orig_stride;
+    a.parity = static_cast<uint8_t *>(d_recovery);
+    a.parity_stripe_stride = rec_stride;
+    a.shard_bytes = sb;
+    a.tabs = static_cast<const RsTab *>(plan->buf->p);
+    a.chunk = plan->chunk;
+    a.n_chunks = plan->n_chunks;
+    a.trunc_first = plan->trunc_first;
+    a.trunc_last = plan->trunc_last;
+    a.m = static_cast<uint32_t>(m);
+    a.k = static_cast<uint32_t>(k);
+    a.tabs_per_chunk = plan->tabs_per_chunk;
+    a.work = plan->work;
+    a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
+    if (kc.variant != Variant::kGeneric) {
+      a.n_stripes = n_stripes;
+      HIP_TRY(launch_encode(kc, a, s));
       return RS_OK;
     }
-  }
-  const KernelChoice kc = choose_encode(k, m, sb, max_nv);
-  EncodeArgs a{};
-  a.data = static_cast<const uint8_t *>(d_original);
-  a.data_stripe_stride = orig_stride;
-  a.parity = static_cast<uint8_t *>(d_recovery);
-  a.parity_stripe_stride = rec_stride;
-  a.shard_bytes = sb;
-  a.tabs = static_cast<const RsTab *>(plan->buf->p);
-  a.chunk = plan->chunk;
-  a.n_chunks = plan->n_chunks;
-  a.trunc_first = plan->trunc_first;
-  a.trunc_last = plan->trunc_last;
-  a.m = static_cast<uint32_t>(m);
-  a.k = static_cast<uint32_t>(k);
-  a.tabs_per_chunk = plan->tabs_per_chunk;
-  a.work = plan->work;
-  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
-  if (kc.variant != Variant::kGeneric) {
-    a.n_stripes = n_stripes;
-    HIP_TRY(launch_encode(kc, a, s));
-    return RS_OK;
-  }
-  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
-  void *scratch = nullptr;
-  HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
-  for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
-    EncodeArgs b = a;
-    b.data += s0 * orig_stride;
-    b.parity += s0 * rec_stride;
-    b.n_stripes = std::min(per, n_stripes - s0);
-    b.scratch = static_cast<uint8_t *>(scratch);
-    b.scratch_stripes = per;
-    hipError_t e = launch_encode(kc, b, s);
-    if (e != hipSuccess) {
-      (void)hipFreeAsync(scratch, s);
-      return hip_fail(e, "launch_encode");
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
+    void *scratch = nullptr;
+    HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
+    for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
+      EncodeArgs b = a;
+      b.data += s0 * orig_stride;
+      b.parity += s0 * rec_stride;
+      b.n_stripes = std::min(per, n_stripes - s0);
+      b.scratch = static_cast<uint8_t *>(scratch);
+      b.scratch_stripes = per;
+      hipError_t e = launch_encode(kc, b, s);
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(scratch, s);
+        return hip_fail(e, "launch_encode");
+      }
     }
-  }
-  HIP_TRY(hipFreeAsync(scratch, s));
-  return RS_OK;
+    HIP_TRY(hipFreeAsync(scratch, s));
+    return RS_OK;
+  });
 }
 
 int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const uint8_t *present,
                              const void *d_original, uint64_t orig_stride, const void *d_recovery,
                              uint64_t rec_stride, void *d_restored, uint64_t out_stride, uint32_t flags,
                              rs_stream_t stream) {
-  if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
-  int st = check_codec(k, m, sb);
-  if (st) return st;
-  uint64_t have = 0, e = 0, have_rec = 0;
-  for (uint64_t i = 0; i < k; i++) {
-    have += present[i] != 0;
-    e += present[i] == 0;
-  }
-  for (uint64_t i = 0; i < m; i++) have_rec += present[k + i] != 0;
-  if (have + have_rec < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
-  if (e == 0 || n_stripes == 0) return RS_OK;  // nothing missing: root.zig:48-57 copy-through
-  if (orig_stride == 0) orig_stride = k * sb;
-  if (rec_stride == 0) rec_stride = m * sb;
-  if (out_stride == 0) out_stride = e * sb;
-  if ((have && !d_original) || (have_rec && !d_recovery) || !d_restored)
-    return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
-  if (sb % 64) {
+  return guarded([&]() -> int {
+    if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    uint64_t have = 0, e = 0, have_rec = 0;
+    for (uint64_t i = 0; i < k; i++) {
+      have += present[i] != 0;
+      e += present[i] == 0;
+    }
+    for (uint64_t i = 0; i < m; i++) have_rec += present[k + i] != 0;
+    if (have + have_rec < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+    if (e == 0 || n_stripes == 0) return RS_OK;  // nothing missing: root.zig:48-57 copy-through
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    if (out_stride == 0) out_stride = e * sb;
+    if ((have && !d_original) || (have_rec && !d_recovery) || !d_restored)
+      return fail(RS_ERR_INVALID_ARGUMENT, "NULL device pointer");
+    if (sb % 64) {
+      int dev;
+      if ((st = current_device(&dev))) return st;
+      return reconstruct_tail(k, m, sb, n_stripes, present, e, static_cast<const uint8_t *>(d_original), orig_stride,
+                              static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
+                              out_stride, flags, static_cast<hipStream_t>(stream));
+    }
+    const int max_nv =
+        align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
+                  reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
+    if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
     int dev;
     if ((st = current_device(&dev))) return st;
-    return reconstruct_tail(k, m, sb, n_stripes, present, e, static_cast<const uint8_t *>(d_original), orig_stride,
+    if (is_low_rate(k, m)) {
+      std::shared_ptr<MapPlan> lp;
+      if ((st = get_low_decode_plan(dev, k, m, flags, present, lp))) return st;
+      return run_map(*lp, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride,
+                     static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored), out_stride,
+                     max_nv, static_cast<hipStream_t>(stream));
+    }
+    std::shared_ptr<DecodePlan> plan;
+    if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
+    if (plan->net && !plan->syndrome && max_nv == 4) {
+      if (const jit::Kernel *nk = net_kernel(*plan->net)) {
+        HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,
                             static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
-                            out_stride, flags, static_cast<hipStream_t>(stream));
-  }
-  const int max_nv =
-      align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
-                reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
-  if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
-  int dev;
-  if ((st = current_device(&dev))) return st;
-  if (is_low_rate(k, m)) {
-    std::shared_ptr<MapPlan> lp;
-    if ((st = get_low_decode_plan(dev, k, m, flags, present, lp))) return st;
-    return run_map(*lp, sb, n_stripes, static_cast<const uint8_t *>(d_original), orig_stride,
-                   static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored), out_stride,
-                   max_nv, static_cast<hipStream_t>(stream));
-  }
-  std::shared_ptr<DecodePlan> plan;
-  if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
-  if (plan->net && !plan->syndrome && max_nv == 4) {
-    if (const jit::Kernel *nk = net_kernel(*plan->net)) {
-      HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,
-                          static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
-                          out_stride, sb, n_stripes, static_cast<hipStream_t>(stream)));
+                            out_stride, sb, n_stripes, static_cast<hipStream_t>(stream)));
+        return RS_OK;
+      }
+    }
+    const KernelChoice kc = plan->tiled    ? choose_decode_mtile(plan->e, sb, max_nv)
+                            : plan->matrix ? choose_decode_matrix(plan->e, sb, max_nv)
+                                           : choose_decode(k, m, sb, max_nv);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const uint8_t *base = static_cast<const uint8_t *>(plan->buf->p);
+    DecodeArgs a{};
+    a.orig = static_cast<const uint8_t *>(d_original);
+    a.orig_stripe_stride = orig_stride;
+    a.rec = static_cast<const uint8_t *>(d_recovery);
+    a.rec_stripe_stride = rec_stride;
+    a.out = static_cast<uint8_t *>(d_restored);
+    a.out_stripe_stride = out_stride;
+    a.shard_bytes = sb;
+    a.tab_ifft = reinterpret_cast<const RsTab *>(base);
+    a.tab_fft = reinterpret_cast<const RsTab *>(base + plan->off_fft);
+    a.tab_pre = reinterpret_cast<const RsTab *>(base + plan->off_pre);
+    a.tab_post = reinterpret_cast<const RsTab *>(base + plan->off_post);
+    a.pos_src = reinterpret_cast<const int32_t *>(base + plan->off_src);
+    a.pos_dst = reinterpret_cast<const int32_t *>(base + plan->off_dst);
+    a.work = plan->work;
+    a.trunc = plan->trunc;
+    a.tab_mat = reinterpret_cast<const RsTab *>(base + plan->off_mat);
+    a.n_in = plan->n_in;
+    a.n_out = plan->e;
+    a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
+    if (!a.orig) a.orig = a.rec;  // never dereferenced for absent shards
+    if (!a.rec) a.rec = a.orig;
+    if (plan->syndrome) {
+      // 1) Enc(d') of the received data (erased shards skipped) into a scratch,
+      // 2) the e x e matrix kernel on the syndromes rec[R_i] ^ scratch[R_i]
+      std::shared_ptr<EncodePlan> ep;
+      if ((st = get_encode_plan(dev, k, m, RS_FLAG_CORRECTED, ep))) return st;
+      const KernelChoice ke = choose_encode(k, m, sb, max_nv);
+      EncodeArgs ea{};
+      ea.data = a.orig;
+      ea.data_stripe_stride = orig_stride;
+      ea.parity_stripe_stride = m * sb;
+      ea.shard_bytes = sb;
+      ea.tabs = static_cast<const RsTab *>(ep->buf->p);
+      ea.chunk = ep->chunk;
+      ea.n_chunks = ep->n_chunks;
+      ea.trunc_first = ep->trunc_first;
+      ea.trunc_last = ep->trunc_last;
+      ea.m = static_cast<uint32_t>(m);
+      ea.k = static_cast<uint32_t>(k);
+      ea.tabs_per_chunk = ep->tabs_per_chunk;
+      ea.work = ep->work;
+      ea.contig = contig_ok(sb, ke.nv);
+      ea.skip = static_cast<const uint32_t *>(plan->skip->p);
+      const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net) : nullptr;
+      const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap * 4 / (m * sb)));
+      void *scratch = nullptr;
+      HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));
+      for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
+        const uint64_t cnt = std::min(per, n_stripes - s0);
+        EncodeArgs eb = ea;
+        eb.data += s0 * orig_stride;
+        eb.parity = static_cast<uint8_t *>(scratch);
+        eb.n_stripes = cnt;
+        DecodeArgs db = a;
+        db.orig += s0 * orig_stride;
+        db.rec += s0 * rec_stride;
+        db.out += s0 * out_stride;
+        db.xsrc = static_cast<const uint8_t *>(scratch);
+        db.xsrc_stripe_stride = m * sb;
+        db.n_stripes = cnt;
+        hipError_t err = launch_encode(ke, eb, s);
+        if (err == hipSuccess) {
+          if (nk)
+            err = jit::launch(*nk, db.orig, orig_stride, db.rec, rec_stride, db.out, out_stride, sb, cnt, s, db.xsrc,
+                              db.xsrc_stripe_stride);
+          else
+            err = launch_decode(kc, db, s);
+        }
+        if (err != hipSuccess) {
+          (void)hipFreeAsync(scratch, s);
+          return hip_fail(err, "syndrome reconstruct");
+        }
+      }
+      HIP_TRY(hipFreeAsync(scratch, s));
       return RS_OK;
     }
-  }
-  const KernelChoice kc = plan->tiled    ? choose_decode_mtile(plan->e, sb, max_nv)
-                          : plan->matrix ? choose_decode_matrix(plan->e, sb, max_nv)
-                                         : choose_decode(k, m, sb, max_nv);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  const uint8_t *base = static_cast<const uint8_t *>(plan->buf->p);
-  DecodeArgs a{};
-  a.orig = static_cast<const uint8_t *>(d_original);
-  a.orig_stripe_stride = orig_stride;
-  a.rec = static_cast<const uint8_t *>(d_recovery);
-  a.rec_stripe_stride = rec_stride;
-  a.out = static_cast<uint8_t *>(d_restored);
-  a.out_stripe_stride = out_stride;
-  a.shard_bytes = sb;
-  a.tab_ifft = reinterpret_cast<const RsTab *>(base);
-  a.tab_fft = reinterpret_cast<const RsTab *>(base + plan->off_fft);
-  a.tab_pre = reinterpret_cast<const RsTab *>(base + plan->off_pre);
-  a.tab_post = reinterpret_cast<const RsTab *>(base + plan->off_post);
-  a.pos_src = reinterpret_cast<const int32_t *>(base + plan->off_src);
-  a.pos_dst = reinterpret_cast<const int32_t *>(base + plan->off_dst);
-  a.work = plan->work;
-  a.trunc = plan->trunc;
-  a.tab_mat = reinterpret_cast<const RsTab *>(base + plan->off_mat);
-  a.n_in = plan->n_in;
-  a.n_out = plan->e;
-  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
-  if (!a.orig) a.orig = a.rec;  // never dereferenced for absent shards
-  if (!a.rec) a.rec = a.orig;
-  if (plan->syndrome) {
-    // 1) Enc(d') of the received data (erased shards skipped) into a scratch,
-    // 2) the e x e matrix kernel on the syndromes rec[R_i] ^ scratch[R_i]
-    std::shared_ptr<EncodePlan> ep;
-    if ((st = get_encode_plan(dev, k, m, RS_FLAG_CORRECTED, ep))) return st;
-    const KernelChoice ke = choose_encode(k, m, sb, max_nv);
-    EncodeArgs ea{};
-    ea.data = a.orig;
-    ea.data_stripe_stride = orig_stride;
-    ea.parity_stripe_stride = m * sb;
-    ea.shard_bytes = sb;
-    ea.tabs = static_cast<const RsTab *>(ep->buf->p);
-    ea.chunk = ep->chunk;
-    ea.n_chunks = ep->n_chunks;
-    ea.trunc_first = ep->trunc_first;
-    ea.trunc_last = ep->trunc_last;
-    ea.m = static_cast<uint32_t>(m);
-    ea.k = static_cast<uint32_t>(k);
-    ea.tabs_per_chunk = ep->tabs_per_chunk;
-    ea.work = ep->work;
-    ea.contig = contig_ok(sb, ke.nv);
-    ea.skip = static_cast<const uint32_t *>(plan->skip->p);
-    const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net) : nullptr;
-    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap * 4 / (m * sb)));
+    if (kc.variant != Variant::kGeneric) {
+      a.n_stripes = n_stripes;
+      HIP_TRY(launch_decode(kc, a, s));
+      return RS_OK;
+    }
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
     void *scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));
+    HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
     for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
-      const uint64_t cnt = std::min(per, n_stripes - s0);
-      EncodeArgs eb = ea;
-      eb.data += s0 * orig_stride;
-      eb.parity = static_cast<uint8_t *>(scratch);
-      eb.n_stripes = cnt;
-      DecodeArgs db = a;
-      db.orig += s0 * orig_stride;
-      db.rec += s0 * rec_stride;
-      db.out += s0 * out_stride;
-      db.xsrc = static_cast<const uint8_t *>(scratch);
-      db.xsrc_stripe_stride = m * sb;
-      db.n_stripes = cnt;
-      hipError_t err = launch_encode(ke, eb, s);
-      if (err == hipSuccess) {
-        if (nk)
-          err = jit::launch(*nk, db.orig, orig_stride, db.rec, rec_stride, db.out, out_stride, sb, cnt, s, db.xsrc,
-                            db.xsrc_stripe_stride);
-        else
-          err = launch_decode(kc, db, s);
-      }
+      DecodeArgs b = a;
+      b.orig += s0 * orig_stride;
+      b.rec += s0 * rec_stride;
+      b.out += s0 * out_stride;
+      b.tab_pre += s0 * a.pattern_stride;
+      b.tab_post += s0 * a.pattern_stride;
+      b.pos_src += s0 * a.pattern_stride;
+      b.pos_dst += s0 * a.pattern_stride;
+      b.n_stripes = std::min(per, n_stripes - s0);
+      b.scratch = static_cast<uint8_t *>(scratch);
+      b.scratch_stripes = per;
+      hipError_t err = launch_decode(kc, b, s);
       if (err != hipSuccess) {
         (void)hipFreeAsync(scratch, s);
-        return hip_fail(err, "syndrome reconstruct");
+        return hip_fail(err, "launch_decode");
       }
     }
     HIP_TRY(hipFreeAsync(scratch, s));
     return RS_OK;
-  }
-  if (kc.variant != Variant::kGeneric) {
-    a.n_stripes = n_stripes;
-    HIP_TRY(launch_decode(kc, a, s));
-    return RS_OK;
-  }
-  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
-  void *scratch = nullptr;
-  HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
-  for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
-    DecodeArgs b = a;
-    b.orig += s0 * orig_stride;
-    b.rec += s0 * rec_stride;
-    b.out += s0 * out_stride;
-    b.tab_pre += s0 * a.pattern_stride;
-    b.tab_post += s0 * a.pattern_stride;
-    b.pos_src += s0 * a.pattern_stride;
-    b.pos_dst += s0 * a.pattern_stride;
-    b.n_stripes = std::min(per, n_stripes - s0);
-    b.scratch = static_cast<uint8_t *>(scratch);
-    b.scratch_stripes = per;
-    hipError_t err = launch_decode(kc, b, s);
-    if (err != hipSuccess) {
-      (void)hipFreeAsync(scratch, s);
-      return hip_fail(err, "launch_decode");
-    }
-  }
-  HIP_TRY(hipFreeAsync(scratch, s));
-  return RS_OK;
+  });
 }
 
 // ------------------------------------------------ per-stripe erasure patterns
@@ -1281,155 +1306,157 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
                                       uint64_t orig_stride, const void *d_recovery, uint64_t rec_stride,
                                       void *d_restored, uint64_t out_stride, int32_t *d_status, uint32_t flags,
                                       rs_stream_t stream) {
-  int st = check_codec(k, m, sb);
-  if (st == RS_OK && is_low_rate(k, m))
-    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "per-stripe patterns: high-rate codes only");
-  if (st) return st;
-  if (n_stripes == 0 || max_e == 0) return RS_OK;
-  if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");
-  if (sb % 64) return fail(RS_ERR_SHARD_TAIL_UNSUPPORTED, "per-stripe patterns need shard_bytes % 64 == 0");
-  if (present_stride == 0) present_stride = k + m;
-  if (orig_stride == 0) orig_stride = k * sb;
-  if (rec_stride == 0) rec_stride = m * sb;
-  if (out_stride == 0) out_stride = static_cast<uint64_t>(max_e) * sb;
-  const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
-                               reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
-  if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
-  int dev;
-  if ((st = current_device(&dev))) return st;
-  const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
-  const uint16_t *dexp, *dlog, *dlw;
-  if ((st = device_tables(dev, &dexp, &dlog, &dlw))) return st;
-  std::shared_ptr<DevBuf> tw;
-  size_t off_fft = 0;
-  if ((st = twiddle_plan(dev, W, flags, tw, off_fft))) return st;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  // matrix path (below): corrected multiply, W <= 32, max_e <= 8
-  const char *pm = std::getenv("RS_AMD_PATTERNS");
-  const bool use_matrix =
-      !(flags & RS_FLAG_QUIRK_D1) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
-  // per-stripe plan: logs u16 | pre RsTab | post RsTab | src i32 | dst i32 (W entries each)
-  //                  [| trimmed present rows, matrix path]
-  const uint64_t per = W * (2 + 2 * sizeof(RsTab) + 8);
-  void *tmp = nullptr;
-  HIP_TRY(hipMallocAsync(&tmp, n_stripes * per + (use_matrix ? n_stripes * (k + m) : 0) + 256, s));
-  if (use_matrix) {  // evaluate the erasure locator for exactly the k inputs the matrix uses
-    uint8_t *trimmed = static_cast<uint8_t *>(tmp) + n_stripes * per;
-    hipError_t e = launch_trim_present(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
-                                       n_stripes, trimmed, s);
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, sb);
+    if (st == RS_OK && is_low_rate(k, m))
+      return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "per-stripe patterns: high-rate codes only");
+    if (st) return st;
+    if (n_stripes == 0 || max_e == 0) return RS_OK;
+    if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");
+    if (sb % 64) return fail(RS_ERR_SHARD_TAIL_UNSUPPORTED, "per-stripe patterns need shard_bytes % 64 == 0");
+    if (present_stride == 0) present_stride = k + m;
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    if (out_stride == 0) out_stride = static_cast<uint64_t>(max_e) * sb;
+    const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
+                                 reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
+    if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
+    const uint16_t *dexp, *dlog, *dlw;
+    if ((st = device_tables(dev, &dexp, &dlog, &dlw))) return st;
+    std::shared_ptr<DevBuf> tw;
+    size_t off_fft = 0;
+    if ((st = twiddle_plan(dev, W, flags, tw, off_fft))) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // matrix path (below): corrected multiply, W <= 32, max_e <= 8
+    const char *pm = std::getenv("RS_AMD_PATTERNS");
+    const bool use_matrix =
+        !(flags & RS_FLAG_QUIRK_D1) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
+    // per-stripe plan: logs u16 | pre RsTab | post RsTab | src i32 | dst i32 (W entries each)
+    //                  [| trimmed present rows, matrix path]
+    const uint64_t per = W * (2 + 2 * sizeof(RsTab) + 8);
+    void *tmp = nullptr;
+    HIP_TRY(hipMallocAsync(&tmp, n_stripes * per + (use_matrix ? n_stripes * (k + m) : 0) + 256, s));
+    if (use_matrix) {  // evaluate the erasure locator for exactly the k inputs the matrix uses
+      uint8_t *trimmed = static_cast<uint8_t *>(tmp) + n_stripes * per;
+      hipError_t e = launch_trim_present(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
+                                         n_stripes, trimmed, s);
+      if (e != hipSuccess) {
+        (void)hipFreeAsync(tmp, s);
+        return hip_fail(e, "launch_trim_present");
+      }
+      d_present = trimmed;
+      present_stride = k + m;
+    }
+    uint8_t *base = static_cast<uint8_t *>(tmp);
+    RsTab *pre = reinterpret_cast<RsTab *>(base);
+    RsTab *post = pre + n_stripes * W;
+    int32_t *src = reinterpret_cast<int32_t *>(post + n_stripes * W);
+    int32_t *dst = src + n_stripes * W;
+    uint16_t *logs = reinterpret_cast<uint16_t *>(dst + n_stripes * W);
+    hipError_t e = launch_pattern_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
+                                       static_cast<uint32_t>(C), static_cast<uint32_t>(W), n_stripes, max_e,
+                                       flags & RS_FLAG_QUIRK_D1, dexp, dlog, dlw, logs, pre, post, src, dst, d_status,
+                                       s);
     if (e != hipSuccess) {
       (void)hipFreeAsync(tmp, s);
-      return hip_fail(e, "launch_trim_present");
+      return hip_fail(e, "launch_pattern_plan");
     }
-    d_present = trimmed;
-    present_stride = k + m;
-  }
-  uint8_t *base = static_cast<uint8_t *>(tmp);
-  RsTab *pre = reinterpret_cast<RsTab *>(base);
-  RsTab *post = pre + n_stripes * W;
-  int32_t *src = reinterpret_cast<int32_t *>(post + n_stripes * W);
-  int32_t *dst = src + n_stripes * W;
-  uint16_t *logs = reinterpret_cast<uint16_t *>(dst + n_stripes * W);
-  hipError_t e = launch_pattern_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
-                                     static_cast<uint32_t>(C), static_cast<uint32_t>(W), n_stripes, max_e,
-                                     flags & RS_FLAG_QUIRK_D1, dexp, dlog, dlw, logs, pre, post, src, dst, d_status,
-                                     s);
-  if (e != hipSuccess) {
-    (void)hipFreeAsync(tmp, s);
-    return hip_fail(e, "launch_pattern_plan");
-  }
-  // Per-stripe e x k matrices built on the GPU, then the matrix kernel (40 MACs per
-  // column for RS(10,4) instead of the FFT reconstruct's 48 multiplies + masks).
-  // Corrected multiply only (under D1 the literal reconstruct uses all received
-  // shards); RS_AMD_PATTERNS=fft keeps the FFT kernels.
-  if (use_matrix) {
-    const uint64_t nk = n_stripes * k;
-    void *mt = nullptr;
-    const uint64_t img_bytes = nk * max_e * 16 * sizeof(uint16_t), tab_bytes = nk * max_e * sizeof(RsTab);
-    e = hipMallocAsync(&mt, tab_bytes + img_bytes + nk * 4 + n_stripes * 4 + 256, s);
-    if (e == hipSuccess) {
-      RsTab *mtabs = static_cast<RsTab *>(mt);
-      uint16_t *images = reinterpret_cast<uint16_t *>(static_cast<uint8_t *>(mt) + tab_bytes);
-      int32_t *srcs = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(mt) + tab_bytes + img_bytes);
-      int32_t *nout = srcs + nk;
-      e = launch_pattern_matrix(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
-                                static_cast<uint32_t>(C), static_cast<uint32_t>(W), n_stripes, max_e, logs,
-                                static_cast<const RsTab *>(tw->p),
-                                reinterpret_cast<const RsTab *>(static_cast<const uint8_t *>(tw->p) + off_fft), dexp,
-                                dlog, images, mtabs, srcs, nout, s);
+    // Per-stripe e x k matrices built on the GPU, then the matrix kernel (40 MACs per
+    // column for RS(10,4) instead of the FFT reconstruct's 48 multiplies + masks).
+    // Corrected multiply only (under D1 the literal reconstruct uses all received
+    // shards); RS_AMD_PATTERNS=fft keeps the FFT kernels.
+    if (use_matrix) {
+      const uint64_t nk = n_stripes * k;
+      void *mt = nullptr;
+      const uint64_t img_bytes = nk * max_e * 16 * sizeof(uint16_t), tab_bytes = nk * max_e * sizeof(RsTab);
+      e = hipMallocAsync(&mt, tab_bytes + img_bytes + nk * 4 + n_stripes * 4 + 256, s);
       if (e == hipSuccess) {
-        const KernelChoice km = choose_decode_matrix(max_e, sb, max_nv);
-        DecodeArgs a{};
-        a.orig = static_cast<const uint8_t *>(d_original);
-        a.orig_stripe_stride = orig_stride;
-        a.rec = static_cast<const uint8_t *>(d_recovery);
-        a.rec_stripe_stride = rec_stride;
-        a.out = static_cast<uint8_t *>(d_restored);
-        a.out_stripe_stride = out_stride;
-        a.shard_bytes = sb;
-        a.tab_mat = mtabs;
-        a.pos_src = srcs;
-        a.n_in = static_cast<uint32_t>(k);
-        a.n_out = max_e;
-        a.mat_stride = k * max_e;
-        a.src_stride = k;
-        a.nout = nout;
-        a.tab_pre = a.tab_post = mtabs;  // unused; launch_decode advances them
-        a.pos_dst = srcs;
-        a.contig = contig_ok(sb, km.nv);
-        a.n_stripes = n_stripes;
-        e = launch_decode(km, a, s);
+        RsTab *mtabs = static_cast<RsTab *>(mt);
+        uint16_t *images = reinterpret_cast<uint16_t *>(static_cast<uint8_t *>(mt) + tab_bytes);
+        int32_t *srcs = reinterpret_cast<int32_t *>(static_cast<uint8_t *>(mt) + tab_bytes + img_bytes);
+        int32_t *nout = srcs + nk;
+        e = launch_pattern_matrix(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
+                                  static_cast<uint32_t>(C), static_cast<uint32_t>(W), n_stripes, max_e, logs,
+                                  static_cast<const RsTab *>(tw->p),
+                                  reinterpret_cast<const RsTab *>(static_cast<const uint8_t *>(tw->p) + off_fft), dexp,
+                                  dlog, images, mtabs, srcs, nout, s);
+        if (e == hipSuccess) {
+          const KernelChoice km = choose_decode_matrix(max_e, sb, max_nv);
+          DecodeArgs a{};
+          a.orig = static_cast<const uint8_t *>(d_original);
+          a.orig_stripe_stride = orig_stride;
+          a.rec = static_cast<const uint8_t *>(d_recovery);
+          a.rec_stripe_stride = rec_stride;
+          a.out = static_cast<uint8_t *>(d_restored);
+          a.out_stripe_stride = out_stride;
+          a.shard_bytes = sb;
+          a.tab_mat = mtabs;
+          a.pos_src = srcs;
+          a.n_in = static_cast<uint32_t>(k);
+          a.n_out = max_e;
+          a.mat_stride = k * max_e;
+          a.src_stride = k;
+          a.nout = nout;
+          a.tab_pre = a.tab_post = mtabs;  // unused; launch_decode advances them
+          a.pos_dst = srcs;
+          a.contig = contig_ok(sb, km.nv);
+          a.n_stripes = n_stripes;
+          e = launch_decode(km, a, s);
+        }
+        (void)hipFreeAsync(mt, s);
       }
-      (void)hipFreeAsync(mt, s);
+      (void)hipFreeAsync(tmp, s);
+      if (e != hipSuccess) return hip_fail(e, "per-stripe matrix reconstruct");
+      return RS_OK;
+    }
+    const KernelChoice kc = choose_decode(k, m, sb, max_nv);
+    DecodeArgs a{};
+    a.orig = static_cast<const uint8_t *>(d_original);
+    a.orig_stripe_stride = orig_stride;
+    a.rec = static_cast<const uint8_t *>(d_recovery);
+    a.rec_stripe_stride = rec_stride;
+    a.out = static_cast<uint8_t *>(d_restored);
+    a.out_stripe_stride = out_stride;
+    a.shard_bytes = sb;
+    a.tab_ifft = static_cast<const RsTab *>(tw->p);
+    a.tab_fft = reinterpret_cast<const RsTab *>(static_cast<const uint8_t *>(tw->p) + off_fft);
+    a.tab_pre = pre;
+    a.tab_post = post;
+    a.pos_src = src;
+    a.pos_dst = dst;
+    a.work = static_cast<uint32_t>(W);
+    a.trunc = static_cast<uint32_t>(C + k);
+    a.pattern_stride = W;
+    a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
+    if (kc.variant != Variant::kGeneric) {
+      a.n_stripes = n_stripes;
+      e = launch_decode(kc, a, s);
+    } else {
+      const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (W * sb)));
+      void *scratch = nullptr;
+      e = hipMallocAsync(&scratch, cap * W * sb, s);
+      for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += cap) {
+        DecodeArgs b = a;
+        b.orig += s0 * orig_stride;
+        b.rec += s0 * rec_stride;
+        b.out += s0 * out_stride;
+        b.tab_pre += s0 * W;
+        b.tab_post += s0 * W;
+        b.pos_src += s0 * W;
+        b.pos_dst += s0 * W;
+        b.n_stripes = std::min(cap, n_stripes - s0);
+        b.scratch = static_cast<uint8_t *>(scratch);
+        e = launch_decode(kc, b, s);
+      }
+      if (scratch) (void)hipFreeAsync(scratch, s);
     }
     (void)hipFreeAsync(tmp, s);
-    if (e != hipSuccess) return hip_fail(e, "per-stripe matrix reconstruct");
+    if (e != hipSuccess) return hip_fail(e, "launch_decode (patterns)");
     return RS_OK;
-  }
-  const KernelChoice kc = choose_decode(k, m, sb, max_nv);
-  DecodeArgs a{};
-  a.orig = static_cast<const uint8_t *>(d_original);
-  a.orig_stripe_stride = orig_stride;
-  a.rec = static_cast<const uint8_t *>(d_recovery);
-  a.rec_stripe_stride = rec_stride;
-  a.out = static_cast<uint8_t *>(d_restored);
-  a.out_stripe_stride = out_stride;
-  a.shard_bytes = sb;
-  a.tab_ifft = static_cast<const RsTab *>(tw->p);
-  a.tab_fft = reinterpret_cast<const RsTab *>(static_cast<const uint8_t *>(tw->p) + off_fft);
-  a.tab_pre = pre;
-  a.tab_post = post;
-  a.pos_src = src;
-  a.pos_dst = dst;
-  a.work = static_cast<uint32_t>(W);
-  a.trunc = static_cast<uint32_t>(C + k);
-  a.pattern_stride = W;
-  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
-  if (kc.variant != Variant::kGeneric) {
-    a.n_stripes = n_stripes;
-    e = launch_decode(kc, a, s);
-  } else {
-    const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (W * sb)));
-    void *scratch = nullptr;
-    e = hipMallocAsync(&scratch, cap * W * sb, s);
-    for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += cap) {
-      DecodeArgs b = a;
-      b.orig += s0 * orig_stride;
-      b.rec += s0 * rec_stride;
-      b.out += s0 * out_stride;
-      b.tab_pre += s0 * W;
-      b.tab_post += s0 * W;
-      b.pos_src += s0 * W;
-      b.pos_dst += s0 * W;
-      b.n_stripes = std::min(cap, n_stripes - s0);
-      b.scratch = static_cast<uint8_t *>(scratch);
-      e = launch_decode(kc, b, s);
-    }
-    if (scratch) (void)hipFreeAsync(scratch, s);
-  }
-  (void)hipFreeAsync(tmp, s);
-  if (e != hipSuccess) return hip_fail(e, "launch_decode (patterns)");
-  return RS_OK;
+  });
 }
 
 // ------------------------------------------------------- host-resident batch
@@ -1512,79 +1539,83 @@ struct Pipelines {
 
 int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const void *h_orig, uint64_t orig_stride,
                          void *h_rec, uint64_t rec_stride, uint32_t flags) {
-  if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
-  int st = check_codec(k, m, sb);
-  if (st) return st;
-  if (n == 0) return RS_OK;
-  if (!h_orig || !h_rec) return fail(RS_ERR_INVALID_ARGUMENT, "NULL host pointer");
-  if (orig_stride == 0) orig_stride = k * sb;
-  if (rec_stride == 0) rec_stride = m * sb;
-  int dev;
-  if ((st = current_device(&dev))) return st;
-  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
-  const int slots = host_slots();
-  Pipeline &p = Pipelines::of(dev);
-  std::lock_guard<std::mutex> lk(p.mu);
-  const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
-  if ((st = p.ensure(bytes, slots))) return st;
-  for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
-    const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
-    const uint64_t cnt = std::min(S, n - s0);
-    hipStream_t q = p.st[slot];
-    HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride, orig_stride,
-                      k * sb, cnt, hipMemcpyHostToDevice, q));
-    if ((st = rs_encode_batch_dev(k, m, sb, cnt, p.buf[slot][0], 0, p.buf[slot][1], 0, flags, q))) return st;
-    HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb, m * sb,
-                      cnt, hipMemcpyDeviceToHost, q));
-  }
-  return p.finish();
+  return guarded([&]() -> int {
+    if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    if (n == 0) return RS_OK;
+    if (!h_orig || !h_rec) return fail(RS_ERR_INVALID_ARGUMENT, "NULL host pointer");
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
+    const int slots = host_slots();
+    Pipeline &p = Pipelines::of(dev);
+    std::lock_guard<std::mutex> lk(p.mu);
+    const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
+    if ((st = p.ensure(bytes, slots))) return st;
+    for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
+      const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
+      const uint64_t cnt = std::min(S, n - s0);
+      hipStream_t q = p.st[slot];
+      HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride, orig_stride,
+                        k * sb, cnt, hipMemcpyHostToDevice, q));
+      if ((st = rs_encode_batch_dev(k, m, sb, cnt, p.buf[slot][0], 0, p.buf[slot][1], 0, flags, q))) return st;
+      HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb, m * sb,
+                        cnt, hipMemcpyDeviceToHost, q));
+    }
+    return p.finish();
+  });
 }
 
 int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const uint8_t *present,
                               const void *h_orig, uint64_t orig_stride, const void *h_rec, uint64_t rec_stride,
                               void *h_out, uint64_t out_stride, uint32_t flags) {
-  if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
-  int st = check_codec(k, m, sb);
-  if (st) return st;
-  uint64_t e = 0, have = 0;
-  for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
-  for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
-  if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
-  if (e == 0 || n == 0) return RS_OK;
-  if (!h_orig || !h_rec || !h_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL host pointer");
-  if (orig_stride == 0) orig_stride = k * sb;
-  if (rec_stride == 0) rec_stride = m * sb;
-  if (out_stride == 0) out_stride = e * sb;
-  int dev;
-  if ((st = current_device(&dev))) return st;
-  const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
-  const int slots = host_slots();
-  Pipeline &p = Pipelines::of(dev);
-  std::lock_guard<std::mutex> lk(p.mu);
-  const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
-  if ((st = p.ensure(bytes, slots))) return st;
-  for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
-    const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
-    const uint64_t cnt = std::min(S, n - s0);
-    hipStream_t q = p.st[slot];
-    // only the present shards cross PCIe
-    for (uint64_t j = 0; j < k; j++)
-      if (present[j])
-        HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + j * sb, k * sb,
-                          static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + j * sb, orig_stride, sb, cnt,
-                          hipMemcpyHostToDevice, q));
-    for (uint64_t j = 0; j < m; j++)
-      if (present[k + j])
-        HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + j * sb, m * sb,
-                          static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + j * sb, rec_stride, sb, cnt,
-                          hipMemcpyHostToDevice, q));
-    if ((st = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
-                                       p.buf[slot][2], 0, flags, q)))
-      return st;
-    HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb, e * sb,
-                      cnt, hipMemcpyDeviceToHost, q));
-  }
-  return p.finish();
+  return guarded([&]() -> int {
+    if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    uint64_t e = 0, have = 0;
+    for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+    for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
+    if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+    if (e == 0 || n == 0) return RS_OK;
+    if (!h_orig || !h_rec || !h_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL host pointer");
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    if (out_stride == 0) out_stride = e * sb;
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
+    const int slots = host_slots();
+    Pipeline &p = Pipelines::of(dev);
+    std::lock_guard<std::mutex> lk(p.mu);
+    const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
+    if ((st = p.ensure(bytes, slots))) return st;
+    for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
+      const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
+      const uint64_t cnt = std::min(S, n - s0);
+      hipStream_t q = p.st[slot];
+      // only the present shards cross PCIe
+      for (uint64_t j = 0; j < k; j++)
+        if (present[j])
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + j * sb, k * sb,
+                            static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + j * sb, orig_stride, sb, cnt,
+                            hipMemcpyHostToDevice, q));
+      for (uint64_t j = 0; j < m; j++)
+        if (present[k + j])
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + j * sb, m * sb,
+                            static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + j * sb, rec_stride, sb, cnt,
+                            hipMemcpyHostToDevice, q));
+      if ((st = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
+                                         p.buf[slot][2], 0, flags, q)))
+        return st;
+      HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb, e * sb,
+                        cnt, hipMemcpyDeviceToHost, q));
+    }
+    return p.finish();
+  });
 }
 
 // ------------------------------------------------------------ one-shot host
@@ -1598,68 +1629,72 @@ struct DevMem {
 }  // namespace
 
 int rs_encode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, uint8_t *const *recovery_out) {
-  if (k == 0 || !original) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "no original shards");  // root.zig:20
-  int st = check_codec(k, m, sb);
-  if (st) return st;
-  for (uint64_t i = 0; i < k; i++)
-    if (!original[i]) return fail(RS_ERR_INVALID_ARGUMENT, "NULL original shard");
-  if (!recovery_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL recovery_out");
-  int dev;
-  if ((st = current_device(&dev))) return st;
-  DevMem din, dout;
-  HIP_TRY(hipMalloc(&din.p, k * sb));
-  HIP_TRY(hipMalloc(&dout.p, m * sb));
-  for (uint64_t i = 0; i < k; i++)
-    HIP_TRY(hipMemcpy(static_cast<uint8_t *>(din.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
-  if ((st = rs_encode_batch_dev(k, m, sb, 1, din.p, 0, dout.p, 0, RS_FLAG_CORRECTED, nullptr))) return st;
-  for (uint64_t r = 0; r < m; r++)
-    HIP_TRY(hipMemcpy(recovery_out[r], static_cast<uint8_t *>(dout.p) + r * sb, sb, hipMemcpyDeviceToHost));
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (k == 0 || !original) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "no original shards");  // root.zig:20
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    for (uint64_t i = 0; i < k; i++)
+      if (!original[i]) return fail(RS_ERR_INVALID_ARGUMENT, "NULL original shard");
+    if (!recovery_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL recovery_out");
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    DevMem din, dout;
+    HIP_TRY(hipMalloc(&din.p, k * sb));
+    HIP_TRY(hipMalloc(&dout.p, m * sb));
+    for (uint64_t i = 0; i < k; i++)
+      HIP_TRY(hipMemcpy(static_cast<uint8_t *>(din.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
+    if ((st = rs_encode_batch_dev(k, m, sb, 1, din.p, 0, dout.p, 0, RS_FLAG_CORRECTED, nullptr))) return st;
+    for (uint64_t r = 0; r < m; r++)
+      HIP_TRY(hipMemcpy(recovery_out[r], static_cast<uint8_t *>(dout.p) + r * sb, sb, hipMemcpyDeviceToHost));
+    return RS_OK;
+  });
 }
 
 int rs_decode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, const uint8_t *const *recovery,
               uint8_t *const *restored_out) {
-  if (!original || !recovery || !restored_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL array");
-  uint64_t orig_present = 0, rec_present = 0;
-  for (uint64_t i = 0; i < k; i++) orig_present += original[i] != nullptr;
-  for (uint64_t i = 0; i < m; i++) rec_present += recovery[i] != nullptr;
-  if (rec_present == 0) {  // root.zig:39-59
-    if (orig_present != k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "no recovery shards and originals incomplete");
-    for (uint64_t i = 0; i < k; i++) std::memcpy(restored_out[i], original[i], sb);
+  return guarded([&]() -> int {
+    if (!original || !recovery || !restored_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL array");
+    uint64_t orig_present = 0, rec_present = 0;
+    for (uint64_t i = 0; i < k; i++) orig_present += original[i] != nullptr;
+    for (uint64_t i = 0; i < m; i++) rec_present += recovery[i] != nullptr;
+    if (rec_present == 0) {  // root.zig:39-59
+      if (orig_present != k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "no recovery shards and originals incomplete");
+      for (uint64_t i = 0; i < k; i++) std::memcpy(restored_out[i], original[i], sb);
+      return RS_OK;
+    }
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    if (orig_present + rec_present < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");  // root.zig:271
+    std::vector<uint8_t> present(k + m);
+    for (uint64_t i = 0; i < k; i++) present[i] = original[i] != nullptr;
+    for (uint64_t i = 0; i < m; i++) present[k + i] = recovery[i] != nullptr;
+    const uint64_t e = k - orig_present;
+    if (e > 0) {
+      int dev;
+      if ((st = current_device(&dev))) return st;
+      DevMem dorig, drec, dout;
+      HIP_TRY(hipMalloc(&dorig.p, k * sb));
+      HIP_TRY(hipMalloc(&drec.p, m * sb));
+      HIP_TRY(hipMalloc(&dout.p, e * sb));
+      for (uint64_t i = 0; i < k; i++)
+        if (original[i])
+          HIP_TRY(hipMemcpy(static_cast<uint8_t *>(dorig.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
+      for (uint64_t i = 0; i < m; i++)
+        if (recovery[i])
+          HIP_TRY(hipMemcpy(static_cast<uint8_t *>(drec.p) + i * sb, recovery[i], sb, hipMemcpyHostToDevice));
+      if ((st = rs_reconstruct_batch_dev(k, m, sb, 1, present.data(), dorig.p, 0, drec.p, 0, dout.p, 0,
+                                         RS_FLAG_CORRECTED, nullptr)))
+        return st;
+      uint64_t slot = 0;
+      for (uint64_t i = 0; i < k; i++)
+        if (!original[i])
+          HIP_TRY(hipMemcpy(restored_out[i], static_cast<uint8_t *>(dout.p) + (slot++) * sb, sb,
+                            hipMemcpyDeviceToHost));
+    }
+    for (uint64_t i = 0; i < k; i++)  // root.zig:76-81
+      if (original[i]) std::memcpy(restored_out[i], original[i], sb);
     return RS_OK;
-  }
-  int st = check_codec(k, m, sb);
-  if (st) return st;
-  if (orig_present + rec_present < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");  // root.zig:271
-  std::vector<uint8_t> present(k + m);
-  for (uint64_t i = 0; i < k; i++) present[i] = original[i] != nullptr;
-  for (uint64_t i = 0; i < m; i++) present[k + i] = recovery[i] != nullptr;
-  const uint64_t e = k - orig_present;
-  if (e > 0) {
-    int dev;
-    if ((st = current_device(&dev))) return st;
-    DevMem dorig, drec, dout;
-    HIP_TRY(hipMalloc(&dorig.p, k * sb));
-    HIP_TRY(hipMalloc(&drec.p, m * sb));
-    HIP_TRY(hipMalloc(&dout.p, e * sb));
-    for (uint64_t i = 0; i < k; i++)
-      if (original[i])
-        HIP_TRY(hipMemcpy(static_cast<uint8_t *>(dorig.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
-    for (uint64_t i = 0; i < m; i++)
-      if (recovery[i])
-        HIP_TRY(hipMemcpy(static_cast<uint8_t *>(drec.p) + i * sb, recovery[i], sb, hipMemcpyHostToDevice));
-    if ((st = rs_reconstruct_batch_dev(k, m, sb, 1, present.data(), dorig.p, 0, drec.p, 0, dout.p, 0,
-                                       RS_FLAG_CORRECTED, nullptr)))
-      return st;
-    uint64_t slot = 0;
-    for (uint64_t i = 0; i < k; i++)
-      if (!original[i])
-        HIP_TRY(hipMemcpy(restored_out[i], static_cast<uint8_t *>(dout.p) + (slot++) * sb, sb,
-                          hipMemcpyDeviceToHost));
-  }
-  for (uint64_t i = 0; i < k; i++)  // root.zig:76-81
-    if (original[i]) std::memcpy(restored_out[i], original[i], sb);
-  return RS_OK;
+  });
 }
 
 // ---------------------------------------------------------------- Encoder
@@ -1671,51 +1706,59 @@ struct rs_encoder {
 };
 
 int rs_encoder_new(uint64_t k, uint64_t m, size_t sb, rs_encoder **out) {
-  if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
-  *out = nullptr;
-  int st = check_codec(k, m, sb);  // root.zig:100-103
-  if (st) return st;
-  try {
-    rs_encoder *e = new rs_encoder;
-    e->k = k;
-    e->m = m;
-    e->sb = sb;
-    e->originals.assign(k * sb, 0);
-    e->recovery.assign(m * sb, 0);
-    *out = e;
-  } catch (...) {
-    return fail(RS_ERR_OUT_OF_MEMORY, "allocation failed");
-  }
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
+    *out = nullptr;
+    int st = check_codec(k, m, sb);  // root.zig:100-103
+    if (st) return st;
+    try {
+      rs_encoder *e = new rs_encoder;
+      e->k = k;
+      e->m = m;
+      e->sb = sb;
+      e->originals.assign(k * sb, 0);
+      e->recovery.assign(m * sb, 0);
+      *out = e;
+    } catch (...) {
+      return fail(RS_ERR_OUT_OF_MEMORY, "allocation failed");
+    }
+    return RS_OK;
+  });
 }
 
 int rs_encoder_add_original_shard(rs_encoder *e, const uint8_t *shard, size_t len) {
-  if (!e || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
-  if (e->received == e->k) return fail(RS_ERR_TOO_MANY_ORIGINAL_SHARDS, "too many original shards");  // root.zig:129
-  if (len != e->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");                // root.zig:130
-  std::memcpy(e->originals.data() + e->received * e->sb, shard, len);
-  e->received++;
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!e || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (e->received == e->k) return fail(RS_ERR_TOO_MANY_ORIGINAL_SHARDS, "too many original shards");  // root.zig:129
+    if (len != e->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");                // root.zig:130
+    std::memcpy(e->originals.data() + e->received * e->sb, shard, len);
+    e->received++;
+    return RS_OK;
+  });
 }
 
 int rs_encoder_encode(rs_encoder *e, const uint8_t **recovery_out) {
-  if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
-  if (e->received != e->k) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "too few original shards");  // root.zig:139
-  std::vector<const uint8_t *> in(e->k);
-  std::vector<uint8_t *> out(e->m);
-  for (uint64_t i = 0; i < e->k; i++) in[i] = e->originals.data() + i * e->sb;
-  for (uint64_t i = 0; i < e->m; i++) out[i] = e->recovery.data() + i * e->sb;
-  int st = rs_encode(e->k, e->m, e->sb, in.data(), out.data());
-  if (st) return st;
-  if (recovery_out)
-    for (uint64_t i = 0; i < e->m; i++) recovery_out[i] = out[i];
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
+    if (e->received != e->k) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "too few original shards");  // root.zig:139
+    std::vector<const uint8_t *> in(e->k);
+    std::vector<uint8_t *> out(e->m);
+    for (uint64_t i = 0; i < e->k; i++) in[i] = e->originals.data() + i * e->sb;
+    for (uint64_t i = 0; i < e->m; i++) out[i] = e->recovery.data() + i * e->sb;
+    int st = rs_encode(e->k, e->m, e->sb, in.data(), out.data());
+    if (st) return st;
+    if (recovery_out)
+      for (uint64_t i = 0; i < e->m; i++) recovery_out[i] = out[i];
+    return RS_OK;
+  });
 }
 
 int rs_encoder_reset(rs_encoder *e) {
-  if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
-  e->received = 0;
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
+    e->received = 0;
+    return RS_OK;
+  });
 }
 
 void rs_encoder_free(rs_encoder *e) { delete e; }
@@ -1730,69 +1773,77 @@ struct rs_decoder {
 };
 
 int rs_decoder_new(uint64_t k, uint64_t m, size_t sb, rs_decoder **out) {
-  if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
-  *out = nullptr;
-  int st = check_codec(k, m, sb);  // root.zig:198-201
-  if (st) return st;
-  try {
-    rs_decoder *d = new rs_decoder;
-    d->k = k;
-    d->m = m;
-    d->sb = sb;
-    d->originals.assign(k * sb, 0);
-    d->recovery.assign(m * sb, 0);
-    d->restored.assign(k * sb, 0);
-    d->have_orig.assign(k, 0);
-    d->have_rec.assign(m, 0);
-    *out = d;
-  } catch (...) {
-    return fail(RS_ERR_OUT_OF_MEMORY, "allocation failed");
-  }
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
+    *out = nullptr;
+    int st = check_codec(k, m, sb);  // root.zig:198-201
+    if (st) return st;
+    try {
+      rs_decoder *d = new rs_decoder;
+      d->k = k;
+      d->m = m;
+      d->sb = sb;
+      d->originals.assign(k * sb, 0);
+      d->recovery.assign(m * sb, 0);
+      d->restored.assign(k * sb, 0);
+      d->have_orig.assign(k, 0);
+      d->have_rec.assign(m, 0);
+      *out = d;
+    } catch (...) {
+      return fail(RS_ERR_OUT_OF_MEMORY, "allocation failed");
+    }
+    return RS_OK;
+  });
 }
 
 // root.zig:236-248
 int rs_decoder_add_original_shard(rs_decoder *d, uint64_t index, const uint8_t *shard, size_t len) {
-  if (!d || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
-  if (index >= d->k) return fail(RS_ERR_INVALID_SHARD_INDEX, "original index out of range");
-  if (d->have_orig[index]) return fail(RS_ERR_DUPLICATE_SHARD_INDEX, "duplicate original index");
-  if (d->orig_received == d->k) return fail(RS_ERR_TOO_MANY_SHARDS, "too many original shards");
-  if (len != d->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");
-  std::memcpy(d->originals.data() + index * d->sb, shard, len);
-  d->have_orig[index] = 1;
-  d->orig_received++;
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!d || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (index >= d->k) return fail(RS_ERR_INVALID_SHARD_INDEX, "original index out of range");
+    if (d->have_orig[index]) return fail(RS_ERR_DUPLICATE_SHARD_INDEX, "duplicate original index");
+    if (d->orig_received == d->k) return fail(RS_ERR_TOO_MANY_SHARDS, "too many original shards");
+    if (len != d->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");
+    std::memcpy(d->originals.data() + index * d->sb, shard, len);
+    d->have_orig[index] = 1;
+    d->orig_received++;
+    return RS_OK;
+  });
 }
 
 // root.zig:250-265
 int rs_decoder_add_recovery_shard(rs_decoder *d, uint64_t index, const uint8_t *shard, size_t len) {
-  if (!d || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
-  if (index >= d->m) return fail(RS_ERR_INVALID_SHARD_INDEX, "recovery index out of range");
-  if (d->have_rec[index]) return fail(RS_ERR_DUPLICATE_SHARD_INDEX, "duplicate recovery index");
-  if (d->rec_received == d->m) return fail(RS_ERR_TOO_MANY_SHARDS, "too many recovery shards");
-  if (len != d->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");
-  std::memcpy(d->recovery.data() + index * d->sb, shard, len);
-  d->have_rec[index] = 1;
-  d->rec_received++;
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!d || !shard) return fail(RS_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (index >= d->m) return fail(RS_ERR_INVALID_SHARD_INDEX, "recovery index out of range");
+    if (d->have_rec[index]) return fail(RS_ERR_DUPLICATE_SHARD_INDEX, "duplicate recovery index");
+    if (d->rec_received == d->m) return fail(RS_ERR_TOO_MANY_SHARDS, "too many recovery shards");
+    if (len != d->sb) return fail(RS_ERR_DIFFERENT_SHARD_SIZE, "shard length differs");
+    std::memcpy(d->recovery.data() + index * d->sb, shard, len);
+    d->have_rec[index] = 1;
+    d->rec_received++;
+    return RS_OK;
+  });
 }
 
 // root.zig:268-335; restored_out[i] points at the original (supplied or restored)
 int rs_decoder_decode(rs_decoder *d, const uint8_t **restored_out) {
-  if (!d) return fail(RS_ERR_INVALID_ARGUMENT, "NULL decoder");
-  if (d->orig_received + d->rec_received < d->k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");
-  std::vector<const uint8_t *> o(d->k), r(d->m);
-  std::vector<uint8_t *> out(d->k);
-  for (uint64_t i = 0; i < d->k; i++) {
-    o[i] = d->have_orig[i] ? d->originals.data() + i * d->sb : nullptr;
-    out[i] = d->restored.data() + i * d->sb;
-  }
-  for (uint64_t i = 0; i < d->m; i++) r[i] = d->have_rec[i] ? d->recovery.data() + i * d->sb : nullptr;
-  int st = rs_decode(d->k, d->m, d->sb, o.data(), r.data(), out.data());
-  if (st) return st;
-  if (restored_out)
-    for (uint64_t i = 0; i < d->k; i++) restored_out[i] = out[i];
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!d) return fail(RS_ERR_INVALID_ARGUMENT, "NULL decoder");
+    if (d->orig_received + d->rec_received < d->k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");
+    std::vector<const uint8_t *> o(d->k), r(d->m);
+    std::vector<uint8_t *> out(d->k);
+    for (uint64_t i = 0; i < d->k; i++) {
+      o[i] = d->have_orig[i] ? d->originals.data() + i * d->sb : nullptr;
+      out[i] = d->restored.data() + i * d->sb;
+    }
+    for (uint64_t i = 0; i < d->m; i++) r[i] = d->have_rec[i] ? d->recovery.data() + i * d->sb : nullptr;
+    int st = rs_decode(d->k, d->m, d->sb, o.data(), r.data(), out.data());
+    if (st) return st;
+    if (restored_out)
+      for (uint64_t i = 0; i < d->k; i++) restored_out[i] = out[i];
+    return RS_OK;
+  });
 }
 
 void rs_decoder_free(rs_decoder *d) { delete d; }
@@ -1821,35 +1872,43 @@ static int engine_transform(uint8_t *shards, uint64_t count, size_t sb, uint64_t
 
 int rs_engine_fft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
                   uint64_t sd, uint32_t flags) {
-  return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, false);
+  return guarded([&]() -> int {
+    return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, false);
+  });
 }
 
 int rs_engine_ifft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
                    uint64_t sd, uint32_t flags) {
-  return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, true);
+  return guarded([&]() -> int {
+    return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, true);
+  });
 }
 
 int rs_engine_mul_scalar(uint8_t *chunks, size_t bytes, uint16_t log_m, uint32_t flags) {
-  if (!chunks) return fail(RS_ERR_INVALID_ARGUMENT, "NULL chunks");
-  if (bytes == 0 || bytes % 64) return fail(RS_ERR_INVALID_SHARD_SIZE, "bytes must be a multiple of 64");
-  int dev, st;
-  if ((st = current_device(&dev))) return st;
-  const RsTab t = make_tab(log_m, flags & RS_FLAG_QUIRK_D1);
-  DevMem dt, dw;
-  HIP_TRY(hipMalloc(&dt.p, sizeof t));
-  HIP_TRY(hipMemcpy(dt.p, &t, sizeof t, hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&dw.p, bytes));
-  HIP_TRY(hipMemcpy(dw.p, chunks, bytes, hipMemcpyHostToDevice));
-  HIP_TRY(launch_mul_scalar(static_cast<uint8_t *>(dw.p), bytes, static_cast<const RsTab *>(dt.p), nullptr));
-  HIP_TRY(hipMemcpy(chunks, dw.p, bytes, hipMemcpyDeviceToHost));
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!chunks) return fail(RS_ERR_INVALID_ARGUMENT, "NULL chunks");
+    if (bytes == 0 || bytes % 64) return fail(RS_ERR_INVALID_SHARD_SIZE, "bytes must be a multiple of 64");
+    int dev, st;
+    if ((st = current_device(&dev))) return st;
+    const RsTab t = make_tab(log_m, flags & RS_FLAG_QUIRK_D1);
+    DevMem dt, dw;
+    HIP_TRY(hipMalloc(&dt.p, sizeof t));
+    HIP_TRY(hipMemcpy(dt.p, &t, sizeof t, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&dw.p, bytes));
+    HIP_TRY(hipMemcpy(dw.p, chunks, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(launch_mul_scalar(static_cast<uint8_t *>(dw.p), bytes, static_cast<const RsTab *>(dt.p), nullptr));
+    HIP_TRY(hipMemcpy(chunks, dw.p, bytes, hipMemcpyDeviceToHost));
+    return RS_OK;
+  });
 }
 
 int rs_engine_eval_poly(uint16_t *erasures, uint64_t trunc) {
-  if (!erasures) return fail(RS_ERR_INVALID_ARGUMENT, "NULL erasures");
-  if (trunc > kOrder) return fail(RS_ERR_INVALID_ARGUMENT, "truncated_size > 65536");
-  eval_poly(erasures, trunc);
-  return RS_OK;
+  return guarded([&]() -> int {
+    if (!erasures) return fail(RS_ERR_INVALID_ARGUMENT, "NULL erasures");
+    if (trunc > kOrder) return fail(RS_ERR_INVALID_ARGUMENT, "truncated_size > 65536");
+    eval_poly(erasures, trunc);
+    return RS_OK;
+  });
 }
 
 }  // extern "C"
