@@ -564,7 +564,14 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
   pending = true;
   if (g_pending.count(key)) return nullptr;
   g_pending.insert(key);
-  g_worker.push(Job{spec, key, dev, tu});
+  try {
+    g_worker.push(Job{spec, key, dev, tu});
+  } catch (const std::exception &ex) {  // no worker thread: the table kernel stays in use
+    g_pending.erase(key);
+    g_failed.emplace(key, std::string("background compile unavailable: ") + ex.what());
+    err = g_failed[key];
+    pending = false;
+  }
   return nullptr;
 }
 
