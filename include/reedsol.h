@@ -169,8 +169,8 @@ const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_cou
 const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                        const uint8_t *present);
 
-/* Large network maps (the e x e syndrome map of wide codes, e.g. RS(200,55) losing 55
- * data shards: ~16-36 s of hipRTC) compile in a background thread; until they are
+/* Large reconstruct network maps (the e x e syndrome map of wide codes, e.g. RS(200,55)
+ * losing 55 data shards: ~16-36 s of hipRTC) compile in a background thread; until they are
  * ready the plan runs its table kernel (same bytes). rs_net_wait blocks until no such
  * compile is running — a service can warm a pattern with one call + rs_net_wait.
  * RS_AMD_JIT_SYNC=1 compiles them in the calling thread instead. Returns RS_OK. */

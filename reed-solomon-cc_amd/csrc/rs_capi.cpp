@@ -252,15 +252,6 @@ void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *pres
 }
 
 // root.zig:136-173 chunk schedule -> table block
-// Encode maps past the synchronous network cap run as a background-compiled network
-// when the table path would be the scratch-walking generic kernel (chunk 32, or > 64):
-// e.g. RS(100,20). Chunk <= 16 and chunk 64 keep their fused table kernels.
-bool encode_net_async(uint64_t k, uint64_t m, uint64_t sb, int max_nv) {
-  return jit::enabled() && !jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb) &&
-         jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb) &&
-         choose_encode(k, m, sb, max_nv).variant == Variant::kGeneric;
-}
-
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out) {
   char key[128];
   std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu/%llu", dev, (unsigned long long)k, (unsigned long long)m,
@@ -289,9 +280,6 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   plan->work = static_cast<uint32_t>((k + C - 1) / C * C);
   if (jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes)) {
     encode_map(k, m, flags, plan->net->spec);
-  } else if (encode_net_async(k, m, jit::kUnitBytes * 64, 4)) {
-    encode_map(k, m, flags, plan->net->spec);  // compiled in the background (rs_jit.hpp)
-    plan->net->async = true;
   }
   g_enc_plans.emplace(key, plan);
   out = plan;
@@ -921,7 +909,6 @@ const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
     return "lowrate_matrix";
   }
   if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name("encode", k, m);
-  if (encode_net_async(k, m, sb, 4)) return net_name("encode", k, m);
   return choose_encode(k, m, sb, 4).name;
 }
 const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const uint8_t *present) {
@@ -1034,8 +1021,7 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
     std::shared_ptr<EncodePlan> plan;
     if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
     if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
-        (plan->net->async ? encode_net_async(k, m, sb, max_nv)
-                          : jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))) {
+        jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
       if (const jit::Kernel *nk = net_kernel(*plan->net)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
                             static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));

@@ -1385,7 +1385,7 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
   (void)k;
   (void)shard_bytes;
   const uint64_t C = ceil_pow2(m);
-  if (C <= 16) {
+  if (C <= 32) {  // C = 32: 64 live slots of one dword pair (NV = 1)
     const int c = static_cast<int>(C);
     const int nv = clamp_nv(std::min(env_nv(4), max_nv), c, true);
     return {Variant::kRegister, c, nv, reg_name(true, c, nv)};
@@ -1507,6 +1507,7 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
     RS_ENC_CASE(4, 1) RS_ENC_CASE(4, 2) RS_ENC_CASE(4, 4)
     RS_ENC_CASE(8, 1) RS_ENC_CASE(8, 2)
     RS_ENC_CASE(16, 1)
+    RS_ENC_CASE(32, 1)
     return hipErrorInvalidValue;
   }
   if (kc.variant == Variant::kWaveSplit) {

@@ -124,15 +124,15 @@ def test_kernel_selection_network():
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"  # more than 16 outputs
     # wide code, 55 erasures: the 55 x 55 syndrome map is a (background-compiled) network
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+net_syndrome_i55_o55"
-    # chunk 32 has no fused table kernel: the encode map compiles in the background
-    assert R.encode_kernel_name(100, 20, 1 << 18) == "net_encode_i100_o20"
+    # chunk 32: the register kernel beats a 300-block network (2.97 vs 3.35 ms)
+    assert R.encode_kernel_name(100, 20, 1 << 18) == "encode_reg_w32_nv1"
 
 
 def test_kernel_selection_async_cap(monkeypatch):
     """RS_AMD_NET_ASYNC_BLOCKS=0 keeps large maps on the table kernels."""
     monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+decode_mtile16_nv1"
-    assert R.encode_kernel_name(100, 20, 1 << 18).startswith("encode_generic")
+    assert R.encode_kernel_name(100, 20, 1 << 18) == "encode_reg_w32_nv1"
 
 
 def test_kernel_selection(monkeypatch):
@@ -150,7 +150,7 @@ def test_kernel_selection(monkeypatch):
     monkeypatch.delenv("RS_AMD_DECODE")
     assert R.reconstruct_kernel_name(200, 55, 320).startswith("decode_generic")
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"
-    assert R.encode_kernel_name(100, 20, 1 << 18).startswith("encode_generic")
+    assert R.encode_kernel_name(100, 20, 1 << 18) == "encode_reg_w32_nv1"
 
 
 def test_net_kernels_compile_for_gfx950():

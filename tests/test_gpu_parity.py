@@ -465,3 +465,27 @@ def test_net_tile_widths_agree(oracle, monkeypatch, k, m):
         torch.cuda.synchronize()
         assert (p.cpu().numpy() == exp).all(), tile
         assert (out.cpu().numpy() == data[:, lost]).all(), tile
+
+
+@pytest.mark.parametrize("k,m", [(100, 20), (30, 30), (40, 17), (33, 32)])
+def test_chunk32_register_encode_vs_oracle(oracle, monkeypatch, k, m):
+    """Chunk 32 (17 <= m <= 32) on the table path: the register kernel
+    k_encode_reg<32,1> (and the syndrome reconstruct built on it), bit-exact."""
+    monkeypatch.setenv("RS_AMD_JIT", "0")
+    assert R.encode_kernel_name(k, m, 4096) == "encode_reg_w32_nv1"
+    rng = np.random.default_rng(k * 7 + m)
+    sb, n = 4096, 2
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = oracle.encode_batch(k, m, data)
+    d = to_dev(data)
+    p = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p)
+    torch.cuda.synchronize()
+    assert (p.cpu().numpy() == exp).all()
+    lost = sorted(int(i) for i in rng.choice(k, size=m, replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    out = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, d, p, out)
+    torch.cuda.synchronize()
+    assert (out.cpu().numpy() == data[:, lost]).all(), R.reconstruct_kernel_name(k, m, sb, present)

@@ -108,27 +108,3 @@ def test_syndrome_network_background_compile(oracle, monkeypatch):
     R.net_wait()
     assert (reconstruct(k, m, present, data, par) == data[:, lost]).all()
 
-
-def test_encode_network_background_compile(oracle, monkeypatch):
-    """RS(100,20): chunk 32 has no fused table kernel, so the encode map (300 network
-    blocks) compiles in the background; generic-kernel calls before, network calls
-    after — both bit-exact against the oracle."""
-    monkeypatch.delenv("RS_AMD_JIT", raising=False)
-    monkeypatch.delenv("RS_AMD_JIT_SYNC", raising=False)
-    k, m, sb, n = 100, 20, 8192, 2
-    rng = np.random.default_rng(10020)
-    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
-    exp = oracle.encode_batch(k, m, data)
-    assert R.encode_kernel_name(k, m, sb) == "net_encode_i100_o20"
-    d = torch.from_numpy(data).to(DEV)
-
-    def enc():
-        p = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
-        R.encode_batch_dev(k, m, d, p)
-        torch.cuda.synchronize()
-        return p.cpu().numpy()
-
-    for _ in range(2):
-        assert (enc() == exp).all()
-    R.net_wait()
-    assert (enc() == exp).all()
