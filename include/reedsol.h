@@ -145,7 +145,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t original_count, uint64_t recovery
 
 /* -------------------------------------- host-resident batches (end to end)
  * Same layouts and semantics as the *_dev calls, but the batch lives in HOST
- * memory: the library streams it through HBM in slices with a 3-deep
+ * memory: the library streams it through HBM in slices on a 2-slot (RS_AMD_HOST_SLOTS)
  * H2D -> kernel -> D2H pipeline on its own streams (PCIe full duplex overlapped
  * with compute) and returns when the results are in host memory. Pinned host
  * buffers (hipHostMalloc / hipHostRegister / torch pin_memory) run at PCIe rate;

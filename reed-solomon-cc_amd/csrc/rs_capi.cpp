@@ -1464,7 +1464,7 @@ hipError_t copy_rows(void *dst, uint64_t dst_stride, const void *src, uint64_t s
 struct Pipeline {
   static constexpr int kMaxSlots = 8;
   std::mutex mu;
-  int slots = 0;  // ring depth in use (RS_AMD_HOST_SLOTS, default 3)
+  int slots = 0;  // ring depth in use (RS_AMD_HOST_SLOTS, default 2)
   hipStream_t st[kMaxSlots] = {};
   void *buf[kMaxSlots][3] = {};
   uint64_t cap[3] = {};
