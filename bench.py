@@ -205,8 +205,8 @@ def main():
                                         "frac": round(v[1] / (v[0] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                                         "data_GiBps": round(data_bytes / (v[0] * 1e-3) / 2**30, 1)}
                                    for kk, v in kinds.items()}}
-        cpu = None
-        if args.cpu_seconds > 0:
+        cpu = None  # host-core baseline: rank 0 at N=1 only (the driver's N>1 runs skip it)
+        if args.cpu_seconds > 0 and world == 1:
             cpu = cpu_baseline(k, m, sb, erase, args.cpu_seconds)
         out = {
             "metric": "device-resident encode+reconstruct GiB/s per GPU (RS(10,4), 1 MiB shards); % HBM roofline",
