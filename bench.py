@@ -131,10 +131,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # local % count: identical on a full node; lets a rehearsal put 2 ranks on 1 GPU
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # nccl (= RCCL) on the node; RS_BENCH_BACKEND=gloo rehearses N>1 on one GPU
+        backend = os.environ.get("RS_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
     k, m, sb, n = args.k, args.m, args.shard_bytes, args.stripes
     erase = [int(x) for x in args.erase.split(",") if x != ""]
     e = len(erase)
