@@ -489,3 +489,21 @@ def test_chunk32_register_encode_vs_oracle(oracle, monkeypatch, k, m):
     R.reconstruct_batch_dev(k, m, present, d, p, out)
     torch.cuda.synchronize()
     assert (out.cpu().numpy() == data[:, lost]).all(), R.reconstruct_kernel_name(k, m, sb, present)
+
+
+@pytest.mark.parametrize("k,m,sb,n_lost", [(1000, 300, 128, 300), (4096, 4096, 64, 2000), (32768, 32768, 64, 4000),
+                                           (65535, 1, 64, 1)])
+def test_maximum_shard_counts_vs_oracle(oracle, k, m, sb, n_lost):
+    """Shard counts up to the codec's limits (root.zig:397-415: chunk + k <= 65536,
+    up to 32768 + 32768 and 65535 + 1): the generic work-buffer kernels with
+    transforms of up to 65,536 points. Encode bit-exact vs the oracle; the
+    reconstruct restores every erased original."""
+    rng = np.random.default_rng(k + m)
+    data = rng.integers(0, 256, (1, k, sb), dtype=np.uint8)
+    par = gpu_encode(k, m, data)
+    np.testing.assert_array_equal(par, oracle.encode_batch(k, m, data))
+    lost = sorted(int(i) for i in rng.choice(k, size=n_lost, replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    rest = gpu_reconstruct(k, m, present, data, par)
+    np.testing.assert_array_equal(rest[0], data[0, lost])
