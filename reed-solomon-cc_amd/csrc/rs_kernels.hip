@@ -1351,6 +1351,18 @@ static int clamp_nv(int nv, int size, bool enc) {
   return nv;
 }
 
+// A wave of the register / matrix kernels covers 512 * NV bytes of a shard: when
+// that leaves more than 1/8 of the lanes idle (small shards), halve NV.
+// RS(32,32) 1 KiB x 65536, 4 erased: decode_matrix_e4 nv4 1.43 -> nv1 0.97 ms.
+static int fit_nv(int nv, uint64_t shard_bytes) {
+  while (nv > 1) {
+    const uint64_t w = 512ull * nv, idle = (shard_bytes + w - 1) / w * w - shard_bytes;
+    if (idle * 8 <= shard_bytes) break;
+    nv >>= 1;
+  }
+  return nv;
+}
+
 static const char *env_variant() { return getenv("RS_AMD_VARIANT"); }
 
 static int env_nv(int dflt) {
@@ -1383,11 +1395,10 @@ static const char *reg_name(bool enc, int size, int nv) {
 
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
   (void)k;
-  (void)shard_bytes;
   const uint64_t C = ceil_pow2(m);
   if (C <= 32) {  // C = 32: 64 live slots of one dword pair (NV = 1)
     const int c = static_cast<int>(C);
-    const int nv = clamp_nv(std::min(env_nv(4), max_nv), c, true);
+    const int nv = clamp_nv(fit_nv(std::min(env_nv(4), max_nv), shard_bytes), c, true);
     return {Variant::kRegister, c, nv, reg_name(true, c, nv)};
   }
   if (C == 64 && shard_bytes % 512 == 0 && (env_variant() == nullptr || std::string(env_variant()) != "generic")) {
@@ -1399,18 +1410,16 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
 }
 
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
-  (void)shard_bytes;
   const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
   if (W <= 32) {
     const int w = static_cast<int>(W);
-    const int nv = clamp_nv(std::min(env_nv(4), max_nv), w, false);
+    const int nv = clamp_nv(fit_nv(std::min(env_nv(4), max_nv), shard_bytes), w, false);
     return {Variant::kRegister, w, nv, reg_name(false, w, nv)};
   }
   return {Variant::kGeneric, static_cast<int>(W), 1, "decode_generic_nv1"};
 }
 
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv) {
-  (void)shard_bytes;
   static const char *kNames[9][3] = {
       {"", "", ""},
       {"decode_matrix_e1_nv1", "decode_matrix_e1_nv2", "decode_matrix_e1_nv4"},
@@ -1421,7 +1430,7 @@ KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_
       {"decode_matrix_e6_nv1", "decode_matrix_e6_nv2", "decode_matrix_e6_nv4"},
       {"decode_matrix_e7_nv1", "decode_matrix_e7_nv2", "decode_matrix_e7_nv4"},
       {"decode_matrix_e8_nv1", "decode_matrix_e8_nv2", "decode_matrix_e8_nv4"}};
-  const int nv = std::min(env_nv(4), max_nv);
+  const int nv = fit_nv(std::min(env_nv(4), max_nv), shard_bytes);
   const int ni = nv == 1 ? 0 : nv == 2 ? 1 : 2;
   KernelChoice kc{Variant::kMatrix, static_cast<int>(n_out), nv, kNames[n_out][ni]};
   const char *pf = getenv("RS_AMD_PREFETCH");  // inputs in flight per lane (1, 2, 4)
