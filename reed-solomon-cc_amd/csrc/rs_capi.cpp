@@ -155,7 +155,8 @@ struct DecodePlan {
 // (the caller then runs the precompiled table-driven kernels).
 // (jit::get caches by content and code-shape knobs; a failure is reported once per plan.)
 // An async slot returns nullptr (table kernels) until its background compile is done.
-const jit::Kernel *net_kernel(NetSlot &slot) {
+// 1 / 2 KiB shards run a variant whose wave units span 4 / 2 stripes (jit::net_pieces).
+const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
   std::lock_guard<std::mutex> lk(slot.mu);
   if (slot.failed) return nullptr;
   std::string err;
@@ -164,7 +165,14 @@ const jit::Kernel *net_kernel(NetSlot &slot) {
     const char *sync = std::getenv("RS_AMD_JIT_SYNC");
     if (!(sync && *sync && std::strcmp(sync, "0") != 0) && ++slot.uses < async_after()) return nullptr;
   }
-  const jit::Kernel *k = slot.async ? jit::get_async(slot.spec, err, pending) : jit::get(slot.spec, err);
+  jit::NetSpec small;
+  const uint32_t pieces = jit::net_pieces(sb);
+  if (pieces > 1) {
+    small = slot.spec;
+    small.pieces = pieces;
+  }
+  const jit::NetSpec &spec = pieces > 1 ? small : slot.spec;
+  const jit::Kernel *k = slot.async ? jit::get_async(spec, err, pending) : jit::get(spec, err);
   if (!k && !pending) {
     slot.failed = true;
     std::fprintf(stderr, "[rs_amd] bit-sliced network unavailable, using table kernels: %s\n", err.c_str());
@@ -441,7 +449,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
-                    std::to_string(jit::enabled() && sb % jit::kUnitBytes == 0 && sb < (1ull << 32)) + "/" +
+                    std::to_string(jit::enabled() && jit::shard_ok(sb)) + "/" +
                     std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
@@ -692,7 +700,7 @@ int run_map(const MapPlan &p, uint64_t sb, uint64_t n, const uint8_t *b0, uint64
   if (!b0) b0 = b1;
   if (!b1) b1 = b0;
   if (max_nv == 4 && jit::enabled() && jit::supports_async(p.n_in, p.n_out, sb))
-    if (const jit::Kernel *nk = net_kernel(*p.net)) {
+    if (const jit::Kernel *nk = net_kernel(*p.net, sb)) {
       HIP_TRY(jit::launch(*nk, b0, s0, b1, s1, out, so, sb, n, s));
       return RS_OK;
     }
@@ -1022,7 +1030,7 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
     if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
     if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
         jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
-      if (const jit::Kernel *nk = net_kernel(*plan->net)) {
+      if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
                             static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));
         return RS_OK;
@@ -1115,7 +1123,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     std::shared_ptr<DecodePlan> plan;
     if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
     if (plan->net && !plan->syndrome && max_nv == 4) {
-      if (const jit::Kernel *nk = net_kernel(*plan->net)) {
+      if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,
                             static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
                             out_stride, sb, n_stripes, static_cast<hipStream_t>(stream)));
@@ -1171,7 +1179,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       ea.work = ep->work;
       ea.contig = contig_ok(sb, ke.nv);
       ea.skip = static_cast<const uint32_t *>(plan->skip->p);
-      const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net) : nullptr;
+      const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net, sb) : nullptr;
       const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap * 4 / (m * sb)));
       void *scratch = nullptr;
       HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));

@@ -114,6 +114,50 @@ __device__ __forceinline__ void st(unsigned char *p, u32 *P) {
 }
 )HIP";
 
+// Small shards (NetSpec::pieces > 1): the four 1 KiB pieces of a wave unit sit in
+// different stripes, so loads and stores take one base pointer per piece. A piece
+// of a stripe past the batch is clamped to the last stripe, which lies in the same
+// unit: it reads the same bytes as that stripe's piece at the same offset, so its
+// store rewrites identical values there (branch-free: guarding the stores with
+// branches made the compiler keep every input's temporaries live, 512 VGPRs + spills).
+const char *kPreludeSmall = R"HIP(
+__device__ __forceinline__ Raw ld4(const unsigned char *const *p, u32 x) {
+  Raw r;
+  r.a0 = LDV(p[0] + x);
+  r.a1 = LDV(p[1] + x);
+  r.b0 = LDV(p[2] + x);
+  r.b1 = LDV(p[3] + x);
+  return r;
+}
+__device__ __forceinline__ Raw ldx4(const unsigned char *const *p, const unsigned char *const *q, u32 x) {
+  Raw r = ld4(p, x);
+  const Raw t = ld4(q, x);
+  r.a0 ^= t.a0;
+  r.a1 ^= t.a1;
+  r.b0 ^= t.b0;
+  r.b1 ^= t.b1;
+  return r;
+}
+__device__ __forceinline__ void st4(unsigned char *const *p, u32 x, u32 *P) {
+  tr8(P);
+  tr8(P + 8);
+  v4 a0, a1, b0, b1;
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const auto s = __builtin_amdgcn_permlane32_swap(P[v], P[8 + v], false, false);
+    const auto t = __builtin_amdgcn_permlane32_swap(P[4 + v], P[12 + v], false, false);
+    a0[v] = s[0];
+    a1[v] = s[1];
+    b0[v] = t[0];
+    b1[v] = t[1];
+  }
+  STV(a0, p[0] + x);
+  STV(a1, p[1] + x);
+  STV(b0, p[2] + x);
+  STV(b1, p[3] + x);
+}
+)HIP";
+
 // XOR network of one input's 16 planes into up to 64 accumulator planes.
 // Four-Russians style: planes in groups of 4; per group every distinct nonzero
 // sub-row a row needs is built once (1 op each from the singles), then every
@@ -234,8 +278,17 @@ uint64_t max_blocks() {
 
 bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
   const uint64_t blocks = static_cast<uint64_t>(n_in) * ((n_out + kTileOut - 1) / kTileOut);
-  return n_in > 0 && n_out > 0 && n_out <= kMaxOut && blocks <= max_blocks() && shard_bytes % kUnitBytes == 0 &&
-         shard_bytes < (1ull << 32);
+  return n_in > 0 && n_out > 0 && n_out <= kMaxOut && blocks <= max_blocks() && shard_ok(shard_bytes);
+}
+
+// RS_AMD_NET_SMALL=0 keeps 1 / 2 KiB shards on the table kernels
+bool shard_ok(uint64_t shard_bytes) {
+  if (shard_bytes == 1024 || shard_bytes == 2048) return env_int("RS_AMD_NET_SMALL", 1) != 0;
+  return shard_bytes > 0 && shard_bytes % kUnitBytes == 0 && shard_bytes < (1ull << 32);
+}
+
+uint32_t net_pieces(uint64_t shard_bytes) {
+  return shard_bytes && shard_bytes < kUnitBytes ? static_cast<uint32_t>(kUnitBytes / shard_bytes) : 1u;
 }
 
 namespace {
@@ -255,13 +308,15 @@ std::string generate_with(const NetSpec &spec, const std::string &name, const Tu
   // several output tiles re-read every input through L2: non-temporal loads (which
   // evict early) cost 10-15 % there, so by default they are kept for 1-tile maps only
   const int nt = std::getenv("RS_AMD_NET_NT") || n_tiles == 1 ? tu.nt : (tu.nt & 2);
+  const uint32_t P = spec.pieces;  // stripes per wave unit (1, or 2 / 4 for 2 / 1 KiB shards)
   o << "#define RS_NT " << nt << "\n" << kPrelude;
+  if (P > 1) o << kPreludeSmall;
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
   if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
   o << "void " << name
     << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
        "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0,\n"
-       "    const unsigned char *__restrict__ b2, u64 s2) {\n"
+       "    const unsigned char *__restrict__ b2, u64 s2, u64 nst) {\n"
        "  const u32 lane = threadIdx.x & 63;\n"
     // XCD-aware: workgroups are dealt round-robin over the 8 XCDs (each with its own
     // L2), so the n_tiles workgroups of one unit group sit 8 apart in blockIdx.x (same
@@ -269,22 +324,48 @@ std::string generate_with(const NetSpec &spec, const std::string &name, const Tu
     << "  const u32 bx = blockIdx.x, tile = (bx / 8u) % " << n_tiles << "u;\n"
     << "  const u64 ugroup = (u64)(bx / 8u / " << n_tiles << "u) * 8u + (bx % 8u);\n"
     << "  const u64 ubase = (ugroup * 4 + (threadIdx.x >> 6)) * " << tu.units << "u;\n"
-       "  const u32 ll = lane & 31;\n"
-       "  const u64 s = stripe0 + blockIdx.y;\n"
-       "  const unsigned char *B0 = b0 + s * s0;\n"
-       "  const unsigned char *B1 = b1 + s * s1;\n"
-       "  const unsigned char *B2 = b2 + s * s2;\n"
-       "  unsigned char *O = out + s * so;\n"
-    << "#pragma unroll 1\n"
-    << "  for (u32 it = 0; it < " << tu.units << "u; it++) {\n"
-       "  const u64 unit = ubase + it;\n"
-       "  if (unit * 4096 >= sb) break;\n"
-       "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n";
+       "  const u32 ll = lane & 31;\n";
+  if (P == 1) {
+    o << "  const u64 s = stripe0 + blockIdx.y;\n"
+         "  const unsigned char *B0 = b0 + s * s0;\n"
+         "  const unsigned char *B1 = b1 + s * s1;\n"
+         "  const unsigned char *B2 = b2 + s * s2;\n"
+         "  unsigned char *O = out + s * so;\n"
+      << "#pragma unroll 1\n"
+      << "  for (u32 it = 0; it < " << tu.units << "u; it++) {\n"
+         "  const u64 unit = ubase + it;\n"
+         "  if (unit * 4096 >= sb) break;\n"
+         "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n";
+  } else {
+    // unit u covers stripes [u*P, u*P + P) of the launch (blockIdx.y == 0); piece i
+    // (1 KiB) lies in stripe u*P + i/(4/P) at shard offset (i % (4/P)) KiB
+    const uint32_t per = 4 / P;  // pieces per stripe
+    o << "#pragma unroll 1\n"
+      << "  for (u32 it = 0; it < " << tu.units << "u; it++) {\n"
+         // wave-uniform (readfirstlane): the piece pointers stay in SGPRs, loads use saddr + voffset
+         "  const u64 unit = (ugroup * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * "
+      << tu.units << "u + it;\n"
+      << "  const u64 sf = stripe0 + unit * " << P << "u;\n"
+         "  if (sf >= nst) break;\n"
+         "  const u32 off = (ll >> 1) * 64u + (lane >= 32 ? 32u : 0u) + (ll & 1) * 16u;\n"
+         "  const unsigned char *B0[4], *B1[4], *B2[4];\n"
+         "  unsigned char *O[4];\n";
+    for (uint32_t i = 0; i < 4; i++) {
+      o << "  { const u64 q = sf + " << i / per << "u;\n"
+        << "    const u64 c = q < nst ? q : nst - 1, po = " << (i % per) * 1024 << "u;\n"
+        << "    B0[" << i << "] = b0 + c * s0 + po; B1[" << i << "] = b1 + c * s1 + po;\n"
+        << "    B2[" << i << "] = b2 + c * s2 + po; O[" << i << "] = out + c * so + po; }\n";
+    }
+  }
   auto load_expr = [&](uint32_t t) {  // ld(shard) or ldx(shard, scratch) for a syndrome input
     const int32_t src = spec.src[t];
     const uint32_t idx = static_cast<uint32_t>(src & kSrcIndexMask);
     std::ostringstream e;
-    if (src & kSrcXorScratch)
+    if (P > 1 && (src & kSrcXorScratch))
+      e << "ldx4(B1, B2, " << idx << "u * (u32)sb + off)";
+    else if (P > 1)
+      e << "ld4(" << ((src & kSrcRecovery) ? "B1" : "B0") << ", " << idx << "u * (u32)sb + off)";
+    else if (src & kSrcXorScratch)
       e << "ldx(B1 + " << idx << "ull * sb + off, B2 + " << idx << "ull * sb + off)";
     else
       e << "ld(" << ((src & kSrcRecovery) ? "B1" : "B0") << " + " << idx << "ull * sb + off)";
@@ -321,7 +402,10 @@ std::string generate_with(const NetSpec &spec, const std::string &name, const Tu
     for (uint32_t jj = 0; jj < nj; jj++) {
       o << "  { u32 Q[16] = {";
       for (int c = 0; c < 16; c++) o << "a" << jj * 16 + c << (c < 15 ? ", " : "};\n");
-      o << "    st(O + " << (j0 + jj) << "ull * sb + off, Q); }\n";
+      if (P > 1)
+        o << "    st4(O, " << (j0 + jj) << "u * (u32)sb + off, Q); }\n";
+      else
+        o << "    st(O + " << (j0 + jj) << "ull * sb + off, Q); }\n";
     }
     o << "  }\n";
   }
@@ -341,7 +425,7 @@ std::set<std::string> g_pending;                          // keys compiling in t
 
 std::string spec_key(const NetSpec &s, int dev, const Tuning &tu) {
   std::string k = std::to_string(dev) + ":" + s.role + ":" + tuning_key(tu) + ":" + std::to_string(s.n_in) + ":" +
-                  std::to_string(s.n_out) + ":";
+                  std::to_string(s.n_out) + ":" + (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "");
   k.append(reinterpret_cast<const char *>(s.src.data()), s.src.size() * sizeof(int32_t));
   k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
   return k;
@@ -393,7 +477,9 @@ bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *co
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
   const Tuning tu = tuning();
-  const std::string name = kernel_name(spec, spec_key(spec, -1, tu)), src = generate_with(spec, name, tu);
+  NetSpec sp = spec;  // RS_AMD_NET_CHECK_PIECES: check the 2 / 4-stripe small-shard variant
+  sp.pieces = static_cast<uint32_t>(std::max(1, std::min(4, env_int("RS_AMD_NET_CHECK_PIECES", 1))));
+  const std::string name = kernel_name(sp, spec_key(sp, -1, tu)), src = generate_with(sp, name, tu);
   if (const char *dir = std::getenv("RS_AMD_JIT_DUMP")) {  // debug aid: keep the generated source
     if (FILE *f = std::fopen((std::string(dir) + "/" + name + ".hip").c_str(), "w")) {
       std::fputs(src.c_str(), f);
@@ -435,6 +521,7 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const
   k->n_out = spec.n_out;
   k->n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
   k->units = static_cast<uint32_t>(tu.units);
+  k->pieces = spec.pieces;
   k->name = name;
   k->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (std::getenv("RS_AMD_JIT_VERBOSE"))
@@ -521,7 +608,7 @@ uint64_t max_async_blocks() {
 bool supports_async(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
   const uint64_t blocks = static_cast<uint64_t>(n_in) * ((n_out + kTileOut - 1) / kTileOut);
   return n_in > 0 && n_out > 0 && n_out <= kMaxOut && blocks <= std::max(max_blocks(), max_async_blocks()) &&
-         shard_bytes % kUnitBytes == 0 && shard_bytes < (1ull << 32);
+         shard_ok(shard_bytes);
 }
 
 const Kernel *get(const NetSpec &spec, std::string &err) {
@@ -583,20 +670,26 @@ void wait_pending() {
 hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const uint8_t *buf1, uint64_t stride1,
                   uint8_t *out, uint64_t out_stride, uint64_t shard_bytes, uint64_t n_stripes, hipStream_t s,
                   const uint8_t *buf2, uint64_t stride2) {
-  const uint64_t units = shard_bytes / kUnitBytes;
+  if (n_stripes == 0) return hipSuccess;
+  if (k.pieces > 1 && shard_bytes * k.pieces != kUnitBytes) return hipErrorInvalidValue;  // wrong kernel for sb
+  // small shards: one launch row whose wave units each span k.pieces stripes
+  const uint64_t units = k.pieces > 1 ? (n_stripes + k.pieces - 1) / k.pieces : shard_bytes / kUnitBytes;
   const uint64_t per_block = 4ull * k.units;
   // unit groups padded to a multiple of 8 (one per XCD, see generate()); the padding
   // workgroups find no unit and exit
   const uint64_t groups = (units + per_block - 1) / per_block;
-  const uint32_t gx = static_cast<uint32_t>((k.n_tiles > 1 ? (groups + 7) / 8 * 8 : groups) * k.n_tiles);
-  for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
-    const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
+  const uint64_t gx64 = (k.n_tiles > 1 ? (groups + 7) / 8 * 8 : groups) * k.n_tiles;
+  if (gx64 > 0x7fffffffull) return hipErrorInvalidValue;
+  const uint32_t gx = static_cast<uint32_t>(gx64);
+  const uint64_t row = k.pieces > 1 ? n_stripes : 65535;  // stripes per launch
+  for (uint64_t s0 = 0; s0 < n_stripes; s0 += row) {
+    const uint32_t gy = k.pieces > 1 ? 1u : static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
     const unsigned char *a0 = buf0, *a1 = buf1 ? buf1 : buf0;
     unsigned char *o = out;
     const unsigned char *a2 = buf2 ? buf2 : a1;
     uint64_t st0 = stride0, st1 = buf1 ? stride1 : stride0, so = out_stride, sb = shard_bytes, first = s0;
-    uint64_t st2 = buf2 ? stride2 : st1;
-    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sb, &first, &a2, &st2};
+    uint64_t st2 = buf2 ? stride2 : st1, nst = n_stripes;
+    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sb, &first, &a2, &st2, &nst};
     hipError_t e = hipModuleLaunchKernel(k.fn, gx, gy, 1, 256, 1, 1, 0, s, args, nullptr);
     if (e != hipSuccess) return e;
   }

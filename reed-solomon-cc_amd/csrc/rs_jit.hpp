@@ -30,6 +30,10 @@ struct NetSpec {
   uint32_t n_in = 0, n_out = 0;
   std::vector<int32_t> src;
   std::vector<uint16_t> images;
+  // stripes per 4 KiB wave unit: 1 (shards of whole 4 KiB units), or 2 / 4 for
+  // 2 KiB / 1 KiB shards, where a wave's four 1 KiB pieces come from that many
+  // consecutive stripes (chosen per launch from the shard size, net_pieces)
+  uint32_t pieces = 1;
 };
 
 // Lanes cover 4 KiB of every shard per wave (32 symbols per lane): shard_bytes
@@ -50,6 +54,11 @@ constexpr uint64_t kMaxAsyncBlocks = 1024;
 uint64_t max_async_blocks();
 bool supports_async(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
 
+// shard sizes the networks cover: whole 4 KiB units below 4 GiB (32-bit lane
+// offsets), or 1 KiB / 2 KiB shards (a wave unit then spans 4 / 2 stripes)
+bool shard_ok(uint64_t shard_bytes);
+uint32_t net_pieces(uint64_t shard_bytes);  // NetSpec::pieces for this shard size
+
 bool enabled();  // RS_AMD_JIT != 0 and hipRTC usable
 bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
 
@@ -59,7 +68,7 @@ std::string generate(const NetSpec &spec, const std::string &name);
 struct Kernel {
   hipModule_t module = nullptr;
   hipFunction_t fn = nullptr;
-  uint32_t n_in = 0, n_out = 0, n_tiles = 0, units = 1;
+  uint32_t n_in = 0, n_out = 0, n_tiles = 0, units = 1, pieces = 1;
   std::string name;
   double compile_ms = 0;
 };

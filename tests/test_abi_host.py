@@ -120,7 +120,9 @@ def test_kernel_selection_network():
     present = [1] * 20
     present[3] = 0
     assert R.reconstruct_kernel_name(16, 4, 8192, present) == "net_reconstruct_i16_o1"
-    assert R.encode_kernel_name(10, 4, 2048) == "encode_reg_w4_nv4"  # not a whole 4 KiB unit
+    assert R.encode_kernel_name(10, 4, 2048) == "net_encode_i10_o4"  # 2 stripes per wave unit
+    assert R.encode_kernel_name(10, 4, 1024) == "net_encode_i10_o4"  # 4 stripes per wave unit
+    assert R.encode_kernel_name(10, 4, 3072) == "encode_reg_w4_nv2"  # not a whole 4 KiB unit
     assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"  # more than 16 outputs
     # wide code, 55 erasures: the 55 x 55 syndrome map is a (background-compiled) network
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+net_syndrome_i55_o55"

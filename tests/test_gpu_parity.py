@@ -507,3 +507,38 @@ def test_maximum_shard_counts_vs_oracle(oracle, k, m, sb, n_lost):
     present[lost] = 0
     rest = gpu_reconstruct(k, m, present, data, par)
     np.testing.assert_array_equal(rest[0], data[0, lost])
+
+
+@pytest.mark.parametrize("sb", [1024, 2048])
+@pytest.mark.parametrize("k,m,n", [(10, 4, 5), (4, 2, 7), (16, 16, 3), (32, 8, 9), (6, 3, 1)])
+def test_small_shard_networks_vs_oracle(oracle, monkeypatch, sb, k, m, n):
+    """1 / 2 KiB shards on the network kernels (wave units span 4 / 2 stripes; stripe
+    counts that are no multiple of that leave pieces past the batch unstored):
+    encode bit-exact vs the oracle, reconstruct restores the erased originals, and
+    the result equals the table kernels' (RS_AMD_NET_SMALL=0)."""
+    assert R.encode_kernel_name(k, m, sb).startswith("net_encode"), R.encode_kernel_name(k, m, sb)
+    rng = np.random.default_rng(k * 131 + m + sb)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = oracle.encode_batch(k, m, data)
+    d = to_dev(data)
+    guard = 0xA5
+    p = torch.full((n + 1, m, sb), guard, dtype=torch.uint8, device=DEV)  # row n: must stay untouched
+    R.encode_batch_dev(k, m, d, p[:n])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(p[:n].cpu().numpy(), exp)
+    assert (p[n].cpu().numpy() == guard).all()
+    lost = sorted(int(i) for i in rng.choice(k, size=min(m, k), replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    assert R.reconstruct_kernel_name(k, m, sb, present).startswith("net_reconstruct")
+    out = torch.full((n + 1, len(lost), sb), guard, dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, d, p[:n], out[:n])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out[:n].cpu().numpy(), data[:, lost])
+    assert (out[n].cpu().numpy() == guard).all()
+    monkeypatch.setenv("RS_AMD_NET_SMALL", "0")
+    assert not R.encode_kernel_name(k, m, sb).startswith("net_")
+    p2 = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p2)
+    torch.cuda.synchronize()
+    assert torch.equal(p2, p[:n])
