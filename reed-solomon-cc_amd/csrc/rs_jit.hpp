@@ -37,7 +37,7 @@ struct NetSpec {
 };
 
 // Lanes cover 4 KiB of every shard per wave (32 symbols per lane): shard_bytes
-// must be a multiple of this, and below 4 GiB (32-bit lane offsets).
+// must be a multiple of this (or 1 / 2 KiB, NetSpec::pieces), below 4 GiB.
 constexpr uint64_t kUnitBytes = 4096;
 constexpr uint32_t kTileOut = 4;      // size caps count blocks of one input x 4 outputs
 constexpr uint32_t kMaxOut = 64;      // tiles of 8 outputs (RS_AMD_NET_TILE), one workgroup each
