@@ -170,3 +170,12 @@ def test_net_kernels_compile_for_gfx950():
     for i in range(0, 64, 2):
         present[i] = 0
     assert R.net_compile_check(200, 55, present) > 0
+
+
+@pytest.mark.parametrize("pieces", ["2", "4"])
+def test_small_shard_net_kernels_compile_for_gfx950(monkeypatch, pieces):
+    """The 2 KiB / 1 KiB-shard network variants (wave units spanning 2 / 4 stripes)
+    compile with hipRTC for gfx950 without a GPU (RS_AMD_NET_CHECK_PIECES)."""
+    monkeypatch.setenv("RS_AMD_NET_CHECK_PIECES", pieces)
+    assert R.net_compile_check(10, 4) > 0
+    assert R.net_compile_check(10, 4, [0, 0, 0, 0] + [1] * 10) > 0
