@@ -183,6 +183,20 @@ int rs_net_wait(void);
 int rs_net_compile_check(uint64_t original_count, uint64_t recovery_count, const uint8_t *present,
                          uint32_t flags, double *compile_ms);
 
+/* Bit-sliced FFT encode kernel (wide codes, chunk 32 / 64): generate
+ * it for (original_count, recovery_count, flags) and compile it with hipRTC, without
+ * loading it (a build check; no device needed). Optional outputs: compile time, code
+ * object bytes, and the generated kernel's VALU instruction estimate per 2 KiB unit
+ * (all waves). RS_ERR_INVALID_ARGUMENT if the code has no such kernel. */
+int rs_fft_compile_check(uint64_t original_count, uint64_t recovery_count, uint32_t flags, double *compile_ms,
+                         uint64_t *code_bytes, uint64_t *valu_ops);
+/* Host check of that kernel's arithmetic (its butterfly schedule with its (u, v)
+ * coordinate matrices on scalar symbols, against the codec's scalar encode, with
+ * the data shards flagged in skip (k bytes, NULL = none) read as zero): *mismatches
+ * = wrong parity symbols over `trials` random stripes. */
+int rs_fft_selftest(uint64_t original_count, uint64_t recovery_count, uint32_t flags, const uint8_t *skip,
+                    int trials, uint64_t *mismatches);
+
 /* ---------------------------------------- Engine seam (Generic.zig), test shim
  * The reference's comptime Engine interface (root.zig:10-12) at per-call
  * granularity, run on the GPU over a HOST buffer of shard_count shards of

@@ -21,6 +21,7 @@
 #include "../../include/reedsol.h"
 #include "rs_gf.hpp"
 #include "rs_internal.hpp"
+#include "rs_fftnet.hpp"
 #include "rs_jit.hpp"
 
 using namespace rs;
@@ -132,10 +133,37 @@ uint32_t async_after() {
   return e && *e ? static_cast<uint32_t>(std::max(1, std::atoi(e))) : 2u;
 }
 
+// Bit-sliced FFT kernel of a plan (rs_fftnet.hpp): wide codes, compiled on first use.
+struct FftSlot {
+  std::mutex mu;
+  bool failed = false;
+  fftnet::Spec spec;
+};
+
+bool fft_enabled() {
+  const char *e = std::getenv("RS_AMD_FFT");
+  return jit::enabled() && !(e && std::strcmp(e, "0") == 0);
+}
+
+const jit::Kernel *fft_kernel(FftSlot &slot) {
+  std::lock_guard<std::mutex> lk(slot.mu);
+  if (slot.failed) return nullptr;
+  std::string err;
+  bool pending = false;
+  const char *a = std::getenv("RS_AMD_FFT_ASYNC");
+  const jit::Kernel *k = fftnet::get(slot.spec, a && *a && std::strcmp(a, "0") != 0, err, pending);
+  if (!k && !pending) {
+    slot.failed = true;
+    std::fprintf(stderr, "[rs_amd] bit-sliced FFT kernel unavailable, using table kernels: %s\n", err.c_str());
+  }
+  return k;
+}
+
 struct EncodePlan {
   std::shared_ptr<DevBuf> buf;
   uint32_t chunk, n_chunks, trunc_first, trunc_last, tabs_per_chunk, work;
   std::shared_ptr<NetSlot> net = std::make_shared<NetSlot>();
+  std::shared_ptr<FftSlot> fft;  // wide codes (chunk 32 / 64)
 };
 
 struct DecodePlan {
@@ -288,6 +316,12 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   plan->work = static_cast<uint32_t>((k + C - 1) / C * C);
   if (jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes)) {
     encode_map(k, m, flags, plan->net->spec);
+  }
+  if (fftnet::supports(k, m, fftnet::kUnitBytes)) {
+    plan->fft = std::make_shared<FftSlot>();
+    plan->fft->spec.k = static_cast<uint32_t>(k);
+    plan->fft->spec.m = static_cast<uint32_t>(m);
+    plan->fft->spec.flags = flags;
   }
   g_enc_plans.emplace(key, plan);
   out = plan;
@@ -916,6 +950,7 @@ const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
       return net_name("encode_low", k, m);
     return "lowrate_matrix";
   }
+  if (fft_enabled() && fftnet::supports(k, m, sb)) return net_name("fft_encode", k, m);
   if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name("encode", k, m);
   return choose_encode(k, m, sb, 4).name;
 }
@@ -960,6 +995,44 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
 int rs_net_wait(void) {
   return guarded([&]() -> int {
     jit::wait_pending();
+    return RS_OK;
+  });
+}
+
+int rs_fft_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compile_ms, uint64_t *code_bytes,
+                         uint64_t *valu_ops) {
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, fftnet::kUnitBytes);
+    if (st) return st;
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
+    fftnet::Spec spec;
+    spec.k = static_cast<uint32_t>(k);
+    spec.m = static_cast<uint32_t>(m);
+    spec.flags = flags;
+    if (valu_ops) {
+      const fftnet::Stats s = fftnet::stats(spec);
+      *valu_ops = s.ops_a + s.ops_b + s.ops_io;
+    }
+    std::string err;
+    size_t bytes = 0;
+    if (!fftnet::compile_check(spec, err, compile_ms, &bytes)) return fail(RS_ERR_DEVICE, err);
+    if (code_bytes) *code_bytes = bytes;
+    return RS_OK;
+  });
+}
+
+int rs_fft_selftest(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *skip, int trials, uint64_t *mismatches) {
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, fftnet::kUnitBytes);
+    if (st) return st;
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
+    fftnet::Spec spec;
+    spec.k = static_cast<uint32_t>(k);
+    spec.m = static_cast<uint32_t>(m);
+    spec.flags = flags;
+    if (skip) spec.skip.assign(skip, skip + k);
+    const uint64_t bad = fftnet::selftest(spec, trials);
+    if (mismatches) *mismatches = bad;
     return RS_OK;
   });
 }
@@ -1028,6 +1101,13 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
     }
     std::shared_ptr<EncodePlan> plan;
     if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
+    if (max_nv == 4 && plan->fft && fft_enabled() && fftnet::supports(k, m, sb)) {
+      if (const jit::Kernel *fk = fft_kernel(*plan->fft)) {
+        HIP_TRY(fftnet::launch(*fk, plan->fft->spec, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
+                               static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));
+        return RS_OK;
+      }
+    }
     if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
         jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
       if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {

@@ -1,0 +1,964 @@
+// rs_fftnet.cpp — generator and launcher of the bit-sliced additive-FFT encode
+// kernels (rs_fftnet.hpp).
+#include "rs_fftnet.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <random>
+#include <sstream>
+
+#include "reedsol.h"
+#include "rs_gf.hpp"
+
+namespace rs {
+namespace fftnet {
+namespace {
+
+// ------------------------------------------------------------------ field side
+// T: Cantor coordinates (lo = beta_0..7, hi = beta_8..15) -> (u, v) with
+// x = u + beta_8 * v, u, v in GF(2^8) = span(beta_0..beta_7) (a Cantor basis spans
+// subfields, gf.zig:8-13). beta_{8+i} = p_i + beta_8 * beta_i, so v = hi and
+// u = lo ^ sum_i hi_i p_i; T is an involution.
+struct Basis {
+  bool ok = false;
+  uint8_t p[8] = {};
+};
+
+const Basis &basis() {
+  static const Basis b = [] {
+    Basis r;
+    const Tables &t = tables();
+    r.ok = true;
+    for (int i = 0; i < 8; i++) {
+      const uint16_t prod = mul16(static_cast<uint16_t>(1u << 8), t.log[1u << i]);  // beta_8 * beta_i
+      const uint16_t pi = static_cast<uint16_t>((1u << (8 + i)) ^ prod);
+      if (pi >> 8) r.ok = false;
+      r.p[i] = static_cast<uint8_t>(pi);
+    }
+    return r;
+  }();
+  return b;
+}
+
+uint16_t to_uv(uint16_t x) {
+  const Basis &b = basis();
+  uint8_t lo = 0;
+  for (int i = 0; i < 8; i++)
+    if (x >> (8 + i) & 1) lo ^= b.p[i];
+  return static_cast<uint16_t>(x ^ lo);
+}
+
+// A twiddle's multiply in (u, v) coordinates: u' = A u + B v, v' = Cm u + D v
+// (row masks: bit j of A[i] = u-input j feeds u-output i). Subfield twiddles have
+// B = Cm = 0 and A = D.
+struct Tw {
+  bool zero = true;  // log 65535: XOR-only butterfly (Generic.zig:38,47,53,103,...)
+  bool sub = false;
+  uint8_t A[8] = {}, B[8] = {}, Cm[8] = {}, D[8] = {};
+};
+
+Tw twiddle(uint16_t log_m, bool d1) {
+  Tw t;
+  if (log_m == kModulus) return t;
+  t.zero = false;
+  for (int j = 0; j < 8; j++) {
+    const uint16_t cu = to_uv(mul_engine(to_uv(static_cast<uint16_t>(1u << j)), log_m, d1));
+    const uint16_t cv = to_uv(mul_engine(to_uv(static_cast<uint16_t>(1u << (8 + j))), log_m, d1));
+    for (int i = 0; i < 8; i++) {
+      t.A[i] |= static_cast<uint8_t>((cu >> i & 1) << j);
+      t.Cm[i] |= static_cast<uint8_t>((cu >> (8 + i) & 1) << j);
+      t.B[i] |= static_cast<uint8_t>((cv >> i & 1) << j);
+      t.D[i] |= static_cast<uint8_t>((cv >> (8 + i) & 1) << j);
+    }
+  }
+  t.sub = true;
+  for (int i = 0; i < 8; i++)
+    if (t.B[i] || t.Cm[i] || t.A[i] != t.D[i]) t.sub = false;
+  return t;
+}
+
+// --------------------------------------------------------------- the schedule
+struct Bf {
+  uint32_t x, y;
+  uint16_t log_m;
+};
+struct Layer {
+  int bit;
+  bool inv;  // IFFT butterfly (y ^= x; x ^= M y) or FFT (x ^= M y; y ^= x)
+  std::vector<Bf> bf;
+};
+
+uint16_t sk(uint64_t idx) { return idx < kModulus ? tables().skew[idx] : static_cast<uint16_t>(kModulus); }
+
+int log2i(uint64_t v) {
+  int b = 0;
+  while ((1ull << b) < v) b++;
+  return b;
+}
+
+// Generic.zig:80-147, group for group (groups r >= trunc skipped as there)
+std::vector<Layer> ifft_layers(uint64_t size, uint64_t trunc, uint64_t sd) {
+  std::vector<Layer> out;
+  uint64_t d = 1;
+  for (uint64_t d4 = 4; d4 <= size; d = d4, d4 <<= 2) {
+    Layer l1{log2i(d), true, {}}, l2{log2i(d) + 1, true, {}};
+    for (uint64_t r = 0; r < trunc; r += d4) {
+      const uint64_t b = r + d + sd - 1;
+      const uint16_t m01 = sk(b), m02 = sk(b + d), m23 = sk(b + 2 * d);
+      for (uint64_t i = r; i < r + d; i++) {
+        l1.bf.push_back({uint32_t(i), uint32_t(i + d), m01});
+        l1.bf.push_back({uint32_t(i + 2 * d), uint32_t(i + 3 * d), m23});
+        l2.bf.push_back({uint32_t(i), uint32_t(i + 2 * d), m02});
+        l2.bf.push_back({uint32_t(i + d), uint32_t(i + 3 * d), m02});
+      }
+    }
+    out.push_back(std::move(l1));
+    out.push_back(std::move(l2));
+  }
+  if (d < size) {  // final odd layer, Generic.zig:131-146
+    Layer l{log2i(d), true, {}};
+    const uint16_t lm = sk(d + sd - 1);
+    for (uint64_t i = 0; i < d; i++) l.bf.push_back({uint32_t(i), uint32_t(d + i), lm});
+    out.push_back(std::move(l));
+  }
+  return out;
+}
+
+// Generic.zig:15-78
+std::vector<Layer> fft_layers(uint64_t size, uint64_t trunc, uint64_t sd) {
+  std::vector<Layer> out;
+  uint64_t d4 = size;
+  for (uint64_t d = size >> 2; d != 0; d4 = d, d >>= 2) {
+    Layer l1{log2i(d) + 1, false, {}}, l2{log2i(d), false, {}};
+    for (uint64_t r = 0; r < trunc; r += d4) {
+      const uint64_t b = r + d + sd - 1;
+      const uint16_t m01 = sk(b), m02 = sk(b + d), m23 = sk(b + 2 * d);
+      for (uint64_t i = r; i < r + d; i++) {
+        l1.bf.push_back({uint32_t(i), uint32_t(i + 2 * d), m02});
+        l1.bf.push_back({uint32_t(i + d), uint32_t(i + 3 * d), m02});
+        l2.bf.push_back({uint32_t(i), uint32_t(i + d), m01});
+        l2.bf.push_back({uint32_t(i + 2 * d), uint32_t(i + 3 * d), m23});
+      }
+    }
+    out.push_back(std::move(l1));
+    out.push_back(std::move(l2));
+  }
+  if (d4 == 2) {  // Generic.zig:64-77
+    Layer l{0, false, {}};
+    for (uint64_t r = 0; r < trunc; r += 2) l.bf.push_back({uint32_t(r), uint32_t(r + 1), sk(r + sd)});
+    out.push_back(std::move(l));
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------- the plan
+// Positions of a chunk: n = log2(C) bits. Layout A: wave = p >> 3, reg = p & 7
+// (bits 0..2 in registers). Layout B: wave = p & (NW - 1), reg = p >> WB.
+struct Plan {
+  uint32_t k = 0, m = 0, C = 0, n = 0, WB = 0, NW = 0;
+  bool d1 = false;
+  std::vector<uint64_t> truncs;
+  std::vector<std::vector<Layer>> ifft;  // per chunk
+  std::vector<Layer> fft;
+  std::vector<std::vector<uint8_t>> valid;  // [chunk][p]: data shard present (not padding, not skipped)
+  std::vector<uint8_t> out_mode;            // [p < C]
+  std::map<uint16_t, Tw> tw;
+
+  uint32_t waveA(uint32_t p) const { return p >> 3; }
+  uint32_t regA(uint32_t p) const { return p & 7; }
+  uint32_t waveB(uint32_t p) const { return p & (NW - 1); }
+  uint32_t regB(uint32_t p) const { return p >> WB; }
+  uint32_t posA(uint32_t w, uint32_t r) const { return (w << 3) | r; }
+  uint32_t posB(uint32_t w, uint32_t t) const { return (t << WB) | w; }
+  bool inA(int bit) const { return bit < 3; }
+  const Tw &get_tw(uint16_t l) {
+    auto it = tw.find(l);
+    if (it == tw.end()) it = tw.emplace(l, twiddle(l, d1)).first;
+    return it->second;
+  }
+};
+
+Plan make_plan(const Spec &s) {
+  Plan p;
+  p.k = s.k;
+  p.m = s.m;
+  p.C = static_cast<uint32_t>(ceil_pow2(s.m));
+  p.n = static_cast<uint32_t>(log2i(p.C));
+  p.WB = p.n - 3;
+  p.NW = 1u << p.WB;
+  p.d1 = (s.flags & RS_FLAG_QUIRK_D1) != 0;
+  p.truncs = encode_chunk_truncs(s.k, s.m, (s.flags & RS_FLAG_QUIRK_D2) != 0);
+  for (size_t j = 0; j < p.truncs.size(); j++) {
+    p.ifft.push_back(ifft_layers(p.C, p.truncs[j], (j + 1) * p.C));  // root.zig:143-166
+    std::vector<uint8_t> v(p.C, 0);
+    for (uint32_t q = 0; q < p.C; q++) {
+      const uint64_t g = j * p.C + q;
+      v[q] = g < s.k && !(g < s.skip.size() && s.skip[g]);
+    }
+    p.valid.push_back(std::move(v));
+  }
+  p.fft = fft_layers(p.C, s.m, 0);  // root.zig:169
+  p.out_mode.assign(p.C, kOutNone);
+  for (uint32_t q = 0; q < s.m; q++) p.out_mode[q] = s.out_mode.empty() ? kOutStore : s.out_mode[q];
+  return p;
+}
+
+// ------------------------------------------------------------------ code gen
+const char *kPrelude = R"HIP(
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef u32 v4 __attribute__((ext_vector_type(4)));
+#define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
+#define MUX(a, b, m) __builtin_amdgcn_bitop3_b32((a), (b), (m), 0xE4)
+#define XM(d, n) __builtin_amdgcn_bitop3_b32((d), (n), 0x0F0F0F0Fu, 0x78)
+#define SWN(a) MUX((a) >> 4, (a) << 4, 0x0F0F0F0Fu)
+#define TRS(j, d, m)                 \
+  {                                  \
+    const u32 a = x[j], b = x[j + d]; \
+    x[j] = MUX(a, b << d, m);        \
+    x[j + d] = MUX(a >> d, b, m);    \
+  }
+__device__ __forceinline__ void tr8(u32 *x) {
+  TRS(0, 4, 0x0F0F0F0Fu) TRS(1, 4, 0x0F0F0F0Fu) TRS(2, 4, 0x0F0F0F0Fu) TRS(3, 4, 0x0F0F0F0Fu)
+  TRS(0, 2, 0x33333333u) TRS(1, 2, 0x33333333u) TRS(4, 2, 0x33333333u) TRS(5, 2, 0x33333333u)
+  TRS(0, 1, 0x55555555u) TRS(2, 1, 0x55555555u) TRS(4, 1, 0x55555555u) TRS(6, 1, 0x55555555u)
+}
+// raw buffer accesses: voffset = the lane's offset in the unit, soffset = the
+// (wave-uniform) shard offset; a resource with 0 records reads zeros
+#define LDB(r, vo, so) __builtin_amdgcn_raw_buffer_load_b128((r), (vo), (so), RS_AUX_LD)
+#define STB(v, r, vo, so) __builtin_amdgcn_raw_buffer_store_b128((v), (r), (vo), (so), RS_AUX_ST)
+// 2 KiB slice of a shard: lanes 0-31 read the lo halves, 32-63 the hi halves of
+// 16 chunks per KiB; one v_permlane32_swap per dword pairs them; then an 8x8 bit
+// transpose per byte lane: P[j] = (lo plane j | hi plane j) per byte (nibbles)
+__device__ __forceinline__ void planes2(v4 a, v4 b, u32 *P) {
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const auto s = __builtin_amdgcn_permlane32_swap(a[v], b[v], false, false);
+    P[v] = s[0];
+    P[4 + v] = s[1];
+  }
+  tr8(P);
+}
+__device__ __forceinline__ void unplanes2(u32 *P, v4 &a, v4 &b) {
+  tr8(P);
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const auto s = __builtin_amdgcn_permlane32_swap(P[v], P[4 + v], false, false);
+    a[v] = s[0];
+    b[v] = s[1];
+  }
+}
+// LDS exchange: slot s = 2 KiB (8 planes x 64 lanes), xch[lq + (s * 8 + i) * 64] holds
+// plane i (dword accesses: no 4-register tuples to assemble); lq = lane, laundered at
+// every exchange so the compiler keeps one base register instead of hoisting an
+// address per slot out of the unit loop
+#define LQ()      \
+  u32 lq = lane; \
+  asm volatile("" : "+v"(lq));
+#define BAR()                                                      \
+  {                                                                \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local"); \
+    __builtin_amdgcn_s_barrier();                                  \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); \
+  }
+)HIP";
+
+int env_int(const char *name, int def) {
+  const char *e = std::getenv(name);
+  return e && *e ? std::atoi(e) : def;
+}
+
+int nt_of() { return env_int("RS_AMD_FFT_NT", 0) & 3; }
+
+int prefetch_of(const Spec &s) {
+  return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", 4)));
+}
+
+struct Gen {
+  std::ostringstream o;
+  int tmp = 0;
+  Stats *st = nullptr;
+  uint64_t *ops = nullptr;  // counter the current section adds to
+
+  std::string fresh(const char *p = "zt") { return p + std::to_string(tmp++); }
+  void op(uint64_t n = 1) {
+    if (ops) *ops += n;
+  }
+
+  // dst[i] (^)= XOR over j in rows[i] of ins[j]; pairs shared by >= 2 rows are
+  // built once (Paar's greedy), each row is then an XOR3 chain.
+  void rows(const std::vector<std::string> &ins, const std::vector<uint32_t> &rowmask,
+            const std::vector<std::string> &dst, bool acc) {
+    std::vector<std::string> names = ins;
+    std::vector<std::vector<int>> r(rowmask.size());
+    for (size_t i = 0; i < rowmask.size(); i++)
+      for (size_t j = 0; j < ins.size(); j++)
+        if (rowmask[i] >> j & 1) r[i].push_back(static_cast<int>(j));
+    for (;;) {
+      std::map<std::pair<int, int>, int> cnt;
+      for (auto &row : r)
+        for (size_t a = 0; a < row.size(); a++)
+          for (size_t b = a + 1; b < row.size(); b++) cnt[{std::min(row[a], row[b]), std::max(row[a], row[b])}]++;
+      std::pair<int, int> best{-1, -1};
+      int bc = 1;
+      for (auto &kv : cnt)
+        if (kv.second > bc) {
+          bc = kv.second;
+          best = kv.first;
+        }
+      if (best.first < 0) break;
+      const std::string nm = fresh();
+      o << "  const u32 " << nm << " = " << names[best.first] << " ^ " << names[best.second] << ";\n";
+      op();
+      const int id = static_cast<int>(names.size());
+      names.push_back(nm);
+      for (auto &row : r) {
+        auto ia = std::find(row.begin(), row.end(), best.first), ib = std::find(row.begin(), row.end(), best.second);
+        if (ia != row.end() && ib != row.end()) {
+          row.erase(std::remove_if(row.begin(), row.end(), [&](int v) { return v == best.first || v == best.second; }),
+                    row.end());
+          row.push_back(id);
+        }
+      }
+    }
+    for (size_t i = 0; i < r.size(); i++) {
+      std::vector<std::string> t;
+      for (int id : r[i]) t.push_back(names[id]);
+      const std::string &d = dst[i];
+      size_t at = 0;
+      if (!acc) {
+        if (t.empty()) {
+          o << "  " << d << " = 0u;\n";
+          continue;
+        }
+        if (t.size() == 1) {
+          o << "  " << d << " = " << t[0] << ";\n";
+          continue;
+        }
+        if (t.size() == 2 || t.size() == 4) {
+          o << "  " << d << " = " << t[0] << " ^ " << t[1] << ";\n";
+          at = 2;
+        } else {
+          o << "  " << d << " = X3(" << t[0] << ", " << t[1] << ", " << t[2] << ");\n";
+          at = 3;
+        }
+        op();
+      }
+      for (; at + 1 < t.size(); at += 2) {
+        o << "  " << d << " = X3(" << d << ", " << t[at] << ", " << t[at + 1] << ");\n";
+        op();
+      }
+      if (at < t.size()) {
+        o << "  " << d << " ^= " << t[at] << ";\n";
+        op();
+      }
+    }
+  }
+
+  static std::vector<std::string> regs(const std::string &pfx) {
+    std::vector<std::string> v;
+    for (int i = 0; i < 8; i++) v.push_back(pfx + "_" + std::to_string(i));
+    return v;
+  }
+
+  // dst (^)= M(src) for a twiddle
+  void mul(const std::vector<std::string> &dst, bool acc, const std::vector<std::string> &src, const Tw &t) {
+    if (t.sub) {
+      if (st) st->subfield++;
+      std::vector<uint32_t> rm(8);
+      for (int i = 0; i < 8; i++) rm[i] = t.A[i];
+      rows(src, rm, dst, acc);
+      return;
+    }
+    if (st) st->general++;
+    // nibble-swapped copies s_j = (v_j | u_j): the low nibble of A y + B s is
+    // A u + B v, the high nibble of D y + Cm s is Cm u + D v
+    std::vector<std::string> ins = src;
+    for (int j = 0; j < 8; j++) {
+      const std::string s = fresh("zs");
+      o << "  const u32 " << s << " = SWN(" << src[j] << ");\n";
+      op(3);
+      ins.push_back(s);
+    }
+    std::vector<uint32_t> rm(16);
+    std::vector<std::string> tl(16);
+    for (int i = 0; i < 8; i++) {
+      rm[i] = t.A[i] | (uint32_t(t.B[i]) << 8);
+      rm[8 + i] = t.D[i] | (uint32_t(t.Cm[i]) << 8);
+      tl[i] = fresh("zl");
+      tl[8 + i] = fresh("zh");
+    }
+    o << "  u32 ";
+    for (int i = 0; i < 16; i++) o << tl[i] << (i < 15 ? ", " : ";\n");
+    rows(ins, rm, tl, false);
+    for (int i = 0; i < 8; i++) {
+      if (acc)
+        o << "  " << dst[i] << " ^= MUX(" << tl[i] << ", " << tl[8 + i] << ", 0x0F0F0F0Fu);\n";
+      else
+        o << "  " << dst[i] << " = MUX(" << tl[i] << ", " << tl[8 + i] << ", 0x0F0F0F0Fu);\n";
+      op(acc ? 2 : 1);
+    }
+  }
+
+  // materialise values here (no sinking of their computation past this point)
+  void pin(const std::vector<std::string> &v) {
+    o << "  asm volatile(\"\" :";
+    for (size_t i = 0; i < v.size(); i++) o << (i ? ", " : " ") << "\"+v\"(" << v[i] << ")";
+    o << ");\n";
+  }
+
+  void copy(const std::vector<std::string> &dst, const std::vector<std::string> &src) {
+    for (int i = 0; i < 8; i++) o << "  " << dst[i] << " = " << src[i] << ";\n";
+  }
+  void xor_into(const std::vector<std::string> &dst, const std::vector<std::string> &src) {
+    for (int i = 0; i < 8; i++) o << "  " << dst[i] << " ^= " << src[i] << ";\n";
+    op(8);
+  }
+
+  int sched = 0;  // sched_barrier after every butterfly (bounds the scheduler's interleaving)
+
+  // one butterfly on named 8-dword positions with zero tracking
+  void butterfly(const std::string &xn, bool &zx, const std::string &yn, bool &zy, bool inv, const Tw &t) {
+    const auto X = regs(xn), Y = regs(yn);
+    if (zx && zy) return;
+    if (sched) o << "  __builtin_amdgcn_sched_barrier(0);\n";
+    if (t.zero && st) st->xor_only++;
+    if (inv) {  // ifftPartial, Generic.zig:171-192: y ^= x; x ^= M y
+      if (!zx) {
+        if (zy)
+          copy(Y, X);
+        else
+          xor_into(Y, X);
+        zy = false;
+      }
+      if (!t.zero && !zy) {
+        mul(X, !zx, Y, t);
+        zx = false;
+      }
+    } else {  // fftPartial, Generic.zig:149-169: x ^= M y; y ^= x
+      if (!t.zero && !zy) {
+        mul(X, !zx, Y, t);
+        zx = false;
+      }
+      if (!zx) {
+        if (zy)
+          copy(Y, X);
+        else
+          xor_into(Y, X);
+        zy = false;
+      }
+    }
+  }
+
+  // Cantor (lo|hi) <-> (u|v) on the 8 dwords of one position (an involution)
+  void basis_change(const std::vector<std::string> &d) {
+    const Basis &b = basis();
+    std::vector<std::string> h(8), nn(8);
+    for (int i = 0; i < 8; i++) {
+      h[i] = fresh("zv");
+      o << "  const u32 " << h[i] << " = " << d[i] << " >> 4;\n";
+      op();
+    }
+    std::vector<uint32_t> rm(8, 0);
+    for (int j = 0; j < 8; j++)
+      for (int i = 0; i < 8; i++)
+        if (b.p[i] >> j & 1) rm[j] |= 1u << i;
+    o << "  u32 ";
+    for (int j = 0; j < 8; j++) {
+      nn[j] = fresh("zn");
+      o << nn[j] << (j < 7 ? ", " : ";\n");
+    }
+    rows(h, rm, nn, false);
+    for (int j = 0; j < 8; j++)
+      if (rm[j]) {
+        o << "  " << d[j] << " = XM(" << d[j] << ", " << nn[j] << ");\n";
+        op();
+      }
+  }
+};
+
+std::string wname(uint32_t r) { return "w" + std::to_string(r); }
+std::string bname(uint32_t t) { return "b" + std::to_string(t); }
+std::string cname(uint32_t t) { return "c" + std::to_string(t); }
+
+// wave-uniform 8-bit masks (one per wave) as a select chain on the wave index
+std::string mask_expr(const std::vector<uint32_t> &per_wave) {
+  bool same = true;
+  for (uint32_t v : per_wave) same &= v == per_wave[0];
+  if (same) return std::to_string(per_wave[0]) + "u";
+  std::string e = "0u";
+  for (size_t w = per_wave.size(); w-- > 0;)
+    e = "(w == " + std::to_string(w) + "u ? " + std::to_string(per_wave[w]) + "u : " + e + ")";
+  return e;
+}
+
+std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
+  Plan P = make_plan(s);
+  Gen g;
+  g.st = stats;
+  g.sched = env_int("RS_AMD_FFT_SCHED", 1);
+  Stats dummy;
+  if (!g.st) g.st = &dummy;
+  std::ostringstream &o = g.o;
+  const uint32_t NW = P.NW, C = P.C;
+  bool any_xor = false;
+  for (uint32_t q = 0; q < s.m; q++) any_xor |= P.out_mode[q] == kOutXorRec;
+  // RS_AMD_FFT_NT: non-temporal loads (bit 0) / stores (bit 1) (cache policy bit nt = 2)
+  const int nt = nt_of();
+  o << "#define RS_AUX_LD " << ((nt & 1) ? 2 : 0) << "\n#define RS_AUX_ST " << ((nt & 2) ? 2 : 0) << "\n" << kPrelude;
+  o << "extern \"C\" __global__ __launch_bounds__(" << NW * 64 << ") void " << name
+    << "(const unsigned char *__restrict__ data, u64 ds, const unsigned char *__restrict__ rec, u64 rs,\n"
+       "    unsigned char *__restrict__ out, u64 os, u32 sb, u32 ups, u64 n_units) {\n"
+    << "  __shared__ u32 xch[" << C * 8 * 64 << "];\n"
+    << "  v4 *const xch4 = (v4 *)xch;\n"
+    << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
+       "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
+       // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division)
+       "  u64 stripe = blockIdx.x / ups;\n"
+       "  u32 uu = blockIdx.x - (u32)stripe * ups;\n"
+       "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n"
+       "  const __amdgpu_buffer_rsrc_t RZ = __builtin_amdgcn_make_buffer_rsrc((void *)data, (short)0, 0, 0x00020000);\n"
+       "  v4 la0[8], lb0[8];\n"
+       "  {  // prologue: the first unit's leading positions of chunk 0\n"
+       "  const u32 sbl = sb, uo = uu * 2048u + loff, uo1 = uo + 1024u;\n"
+    << "  const __amdgpu_buffer_rsrc_t RD = blockIdx.x < n_units ? __builtin_amdgcn_make_buffer_rsrc((void *)(data + "
+       "stripe * ds), (short)0, (int)("
+    << s.k << "u * sbl), 0x00020000) : RZ;\n";
+  // (loads emitted below, once emit_loads exists)
+  std::ostringstream hdr2;
+  hdr2 << "#pragma unroll 1\n"
+       "  for (u64 u = blockIdx.x; u < n_units; u += gridDim.x) {\n"
+       "  u32 sbl = sb;\n"
+       "  asm volatile(\"\" : \"+s\"(sbl));  // shard offsets are recomputed per unit (SALU), not hoisted into VGPRs\n"
+       "  const u32 uo = uu * 2048u + loff, uo1 = uo + 1024u;\n"
+    << "  const __amdgpu_buffer_rsrc_t RD = __builtin_amdgcn_make_buffer_rsrc((void *)(data + stripe * ds), (short)0, (int)("
+    << s.k << "u * sbl), 0x00020000);\n"
+    << "  const __amdgpu_buffer_rsrc_t RO = __builtin_amdgcn_make_buffer_rsrc((void *)(out + stripe * os), (short)0, (int)("
+    << s.m << "u * sbl), 0x00020000);\n";
+  if (any_xor)
+    hdr2 << "  const __amdgpu_buffer_rsrc_t RR = __builtin_amdgcn_make_buffer_rsrc((void *)(rec + stripe * rs), (short)0, "
+         "(int)("
+      << s.m << "u * sbl), 0x00020000);\n";
+  hdr2 << "  u32 ";
+  for (uint32_t r = 0; r < 8; r++)
+    for (int i = 0; i < 8; i++) hdr2 << "w" << r << "_" << i << ", b" << r << "_" << i << ", c" << r << "_" << i << (r == 7 && i == 7 ? ";\n" : ", ");
+
+  // LDS slot accesses (RS_AMD_FFT_LDS128: 4-dword accesses, planes 4q..4q+3 of a slot
+  // in quad q; else dword accesses, plane i at (s * 8 + i) * 64)
+  const bool l128 = env_int("RS_AMD_FFT_LDS128", 0) != 0;
+  auto lds_write = [&](const std::string &wexpr, uint32_t slot, const std::vector<std::string> &v) {
+    // slot address = wexpr (runtime, in slots) + slot
+    for (int q = 0; q < (l128 ? 2 : 8); q++) {
+      if (l128)
+        o << "  xch4[lq + " << wexpr << " * 128u + " << slot * 128 + q * 64 << "u] = (v4){" << v[4 * q] << ", "
+          << v[4 * q + 1] << ", " << v[4 * q + 2] << ", " << v[4 * q + 3] << "};\n";
+      else
+        o << "  xch[lq + " << wexpr << " * 512u + " << (slot * 8 + q) * 64 << "u] = " << v[q] << ";\n";
+    }
+  };
+  auto lds_read = [&](const std::string &wexpr, uint32_t slot, const std::vector<std::string> &v) {
+    if (l128) {
+      o << "  { const v4 q0 = xch4[lq + " << wexpr << " * 128u + " << slot * 128 << "u], q1 = xch4[lq + " << wexpr
+        << " * 128u + " << slot * 128 + 64 << "u];\n";
+      for (int i = 0; i < 4; i++) o << "  " << v[i] << " = q0[" << i << "]; " << v[4 + i] << " = q1[" << i << "];\n";
+      o << "  }\n";
+    } else {
+      for (int i = 0; i < 8; i++)
+        o << "  " << v[i] << " = xch[lq + " << wexpr << " * 512u + " << (slot * 8 + i) * 64 << "u];\n";
+    }
+  };
+
+  // ---- loads of chunk j (layout A: wave w reads positions w*8 + r), raw into la/lb
+  std::vector<uint8_t> declared(P.truncs.size(), 0);
+  auto emit_loads = [&](size_t j, uint32_t r0, uint32_t r1, const char *rd = "RD", const char *uo0 = "uo",
+                        const char *uo1 = "uo1") {
+    std::vector<uint32_t> vm(NW, 0);
+    bool full = true;
+    for (uint32_t w = 0; w < NW; w++)
+      for (uint32_t r = 0; r < 8; r++) {
+        if (P.valid[j][P.posA(w, r)]) vm[w] |= 1u << r;
+        else full = false;
+      }
+    if (!declared[j]) o << "  v4 la" << j << "[8], lb" << j << "[8];\n";
+    declared[j] = 1;
+    if (r0 == r1) return vm;
+    o << "  __builtin_amdgcn_sched_barrier(0);\n  {\n";
+    if (!full) o << "  const u32 vm = " << mask_expr(vm) << ";\n";
+    for (uint32_t r = r0; r < r1; r++) {
+      o << "  { const u32 so = (" << j * C + r << "u + (w << 3)) * sbl;\n    ";
+      const std::string rs = full ? std::string(rd) : "((vm >> " + std::to_string(r) + " & 1u) ? " + rd + " : RZ)";
+      o << "la" << j << "[" << r << "] = LDB(" << rs << ", " << uo0 << ", so); lb" << j << "[" << r << "] = LDB(" << rs
+        << ", " << uo1 << ", so); }\n";
+    }
+    o << "  }\n  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_sched_barrier(0);\n";
+    return vm;
+  };
+
+  std::vector<uint8_t> acc_live(8, 0);  // layout B regs of the accumulator
+  // RS_AMD_FFT_PREFETCH: positions of the next chunk loaded before this chunk's layers
+  // (the rest just before their plane transform)
+  const uint32_t pf = static_cast<uint32_t>(prefetch_of(s));
+  // RS_AMD_FFT_XUNIT: the next unit's first pf positions are loaded during this unit's FFT
+  const bool xunit = env_int("RS_AMD_FFT_XUNIT", 1) != 0;
+  declared[0] = 1;  // la0 / lb0 live across units (cross-unit prefetch)
+  std::vector<uint32_t> vm_next = emit_loads(0, 0, xunit ? pf : 0);
+  o << "  }\n" << hdr2.str();
+  emit_loads(0, xunit ? pf : 0, 8);
+  for (size_t j = 0; j < P.truncs.size(); j++) {
+    const std::vector<uint32_t> vm = vm_next;
+    if (j > 0) emit_loads(j, pf, 8);
+    o << "  // ---- chunk " << j << " (data shards " << j * C << "..): IFFT(size " << C << ", trunc " << P.truncs[j]
+      << ", skew_delta " << (j + 1) * C << "), Generic.zig:80-147\n";
+    // planes + basis change (shared code; invalid positions were read as zeros)
+    g.ops = &g.st->ops_io;
+    for (uint32_t r = 0; r < 8; r++) {
+      bool any = false;
+      for (uint32_t w = 0; w < NW; w++) any |= (vm[w] >> r & 1) != 0;
+      if (!any) continue;
+      o << "  { u32 Q[8]; planes2(la" << j << "[" << r << "], lb" << j << "[" << r << "], Q);\n";
+      for (int i = 0; i < 8; i++) o << "  w" << r << "_" << i << " = Q[" << i << "];\n";
+      g.op(4 + 48);
+      const auto W = Gen::regs(wname(r));
+      g.basis_change(W);
+      o << "  }\n";
+    }
+    if (j + 1 < P.truncs.size()) vm_next = emit_loads(j + 1, 0, pf);  // in flight during this chunk's layers
+    // ---- layout A layers (bits 0..2), specialised per wave; liveness first
+    std::vector<std::vector<uint8_t>> liveA(NW, std::vector<uint8_t>(8, 0));
+    for (uint32_t w = 0; w < NW; w++) {
+      bool z[8];
+      for (uint32_t r = 0; r < 8; r++) z[r] = !(vm[w] >> r & 1);
+      for (const Layer &L : P.ifft[j]) {
+        if (!P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf)
+          if (P.waveA(b.x) == w && !(z[P.regA(b.x)] && z[P.regA(b.y)])) z[P.regA(b.x)] = z[P.regA(b.y)] = false;
+      }
+      for (uint32_t r = 0; r < 8; r++) liveA[w][r] = !z[r];
+    }
+    std::vector<uint8_t> liveB(8, 0);
+    for (uint32_t w = 0; w < NW; w++)
+      for (uint32_t r = 0; r < 8; r++)
+        if (liveA[w][r]) liveB[P.regB(P.posA(w, r))] = 1;
+    // A layers, then A -> B through LDS: A wave a writes reg r (position p) to slot
+    // (p & (NW-1)) * 8 + (p >> WB); the slots are free (every wave passed the barrier
+    // after the previous exchange's reads)
+    g.ops = &g.st->ops_a;
+    o << "  {\n  LQ();\n";
+    for (uint32_t w = 0; w < NW; w++) {
+      bool z[8];
+      for (uint32_t r = 0; r < 8; r++) z[r] = !(vm[w] >> r & 1);
+      o << "  " << (w ? "else if" : "if") << " (w == " << w << "u) {\n";
+      for (const Layer &L : P.ifft[j]) {
+        if (!P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf) {
+          if (P.waveA(b.x) != w) continue;
+          const uint32_t rx = P.regA(b.x), ry = P.regA(b.y);
+          g.butterfly(wname(rx), z[rx], wname(ry), z[ry], true, P.get_tw(b.log_m));
+        }
+      }
+      for (uint32_t r = 0; r < 8; r++) {
+        const uint32_t p = P.posA(w, r), t = P.regB(p);
+        if (!liveB[t]) continue;
+        const uint32_t slot = P.waveB(p) * 8 + t;
+        std::vector<std::string> v = Gen::regs(wname(r));
+        if (z[r]) v.assign(8, "0u");
+        lds_write("0", slot, v);
+      }
+      o << "  }\n";
+    }
+    o << "  BAR();\n";
+    bool zb[8];
+    for (uint32_t t = 0; t < 8; t++) {
+      zb[t] = !liveB[t];
+      if (!liveB[t]) continue;
+      lds_read("(w * 8u)", t, Gen::regs(bname(t)));
+    }
+    o << "  BAR();\n  }\n";  // every wave has read its slots: the next exchange may write
+    // ---- layout B layers (bits >= 3), one code path for all waves
+    g.ops = &g.st->ops_b;
+    for (const Layer &L : P.ifft[j]) {
+      if (P.inA(L.bit)) continue;
+      for (const Bf &b : L.bf) {
+        if (P.waveB(b.x) != 0) continue;  // twiddles are uniform over the wave bits
+        const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+        g.butterfly(bname(tx), zb[tx], bname(ty), zb[ty], true, P.get_tw(b.log_m));
+      }
+    }
+    // XOR-fold into the accumulator, root.zig:150-166
+    for (uint32_t t = 0; t < 8; t++) {
+      if (zb[t]) continue;
+      if (acc_live[t])
+        g.xor_into(Gen::regs(cname(t)), Gen::regs(bname(t)));
+      else
+        g.copy(Gen::regs(cname(t)), Gen::regs(bname(t)));
+      acc_live[t] = 1;
+    }
+    for (uint32_t t = 0; t < 8; t++)
+      if (acc_live[t]) g.pin(Gen::regs(cname(t)));
+    o << "  __builtin_amdgcn_sched_barrier(0);\n  asm volatile(\"\" ::: \"memory\");\n";
+  }
+
+  // ---- FFT(size C, trunc m, skew_delta 0), Generic.zig:15-78 — needed positions first
+  std::vector<uint8_t> need(C, 0);  // at the start of the A layers
+  {
+    std::vector<uint8_t> nd(C, 0);
+    for (uint32_t q = 0; q < C; q++) nd[q] = P.out_mode[q] != kOutNone;
+    for (auto it = P.fft.rbegin(); it != P.fft.rend(); ++it) {
+      if (!P.inA(it->bit)) continue;
+      for (const Bf &b : it->bf)
+        if (nd[b.x] || nd[b.y]) nd[b.x] = nd[b.y] = 1;
+    }
+    need = nd;
+  }
+  o << "  // ---- FFT(size " << C << ", trunc " << s.m << ", skew_delta 0), Generic.zig:15-78\n";
+  g.ops = &g.st->ops_b;
+  bool zc[8];
+  for (uint32_t t = 0; t < 8; t++) zc[t] = !acc_live[t];
+  for (const Layer &L : P.fft) {
+    if (P.inA(L.bit)) continue;
+    for (const Bf &b : L.bf) {
+      if (P.waveB(b.x) != 0) continue;
+      const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+      g.butterfly(cname(tx), zc[tx], cname(ty), zc[ty], false, P.get_tw(b.log_m));
+    }
+  }
+  // the next unit's leading chunk-0 positions, in flight during this unit's last exchange and stores
+  o << "  u64 stripe_n = stripe + gdiv;\n  u32 uu_n = uu + gmod;\n  if (uu_n >= ups) { uu_n -= ups; stripe_n++; }\n";
+  if (pf && xunit) {
+    o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = uon + 1024u;\n"
+      << "  const __amdgpu_buffer_rsrc_t RDn = u + gridDim.x < n_units ? __builtin_amdgcn_make_buffer_rsrc((void *)(data + "
+         "stripe_n * ds), (short)0, (int)("
+      << s.k << "u * sbl), 0x00020000) : RZ;\n";
+    emit_loads(0, 0, pf, "RDn", "uon", "uon1");
+    o << "  }\n";
+  }
+  // B -> A: B wave w writes reg t (position p = t << WB | w) to slot p; then every
+  // wave reads its 8 slots (shared code) and passes a barrier before the
+  // specialised A layers, so the next unit's first exchange may write at once
+  std::vector<uint8_t> needB(8, 0);
+  for (uint32_t q = 0; q < C; q++)
+    if (need[q]) needB[P.regB(q)] = 1;
+  std::vector<uint8_t> readA(8, 0);
+  for (uint32_t q = 0; q < C; q++)
+    if (need[q] && !zc[P.regB(q)]) readA[P.regA(q)] = 1;
+  o << "  {\n  LQ();\n";
+  for (uint32_t t = 0; t < 8; t++) {
+    if (!needB[t] || zc[t]) continue;
+    lds_write("w", t << P.WB, Gen::regs(cname(t)));
+  }
+  o << "  BAR();\n";
+  for (uint32_t r = 0; r < 8; r++) {
+    if (!readA[r]) continue;
+    lds_read("(w * 8u)", r, Gen::regs(wname(r)));
+  }
+  o << "  BAR();\n  }\n";
+  g.ops = &g.st->ops_a;
+  bool first = true;
+  for (uint32_t w = 0; w < NW; w++) {
+    bool anyout = false;
+    for (uint32_t r = 0; r < 8; r++) anyout |= P.out_mode[P.posA(w, r)] != kOutNone;
+    if (!anyout) continue;
+    o << "  " << (first ? "if" : "else if") << " (w == " << w << "u) {\n";
+    first = false;
+    bool z[8];
+    for (uint32_t r = 0; r < 8; r++) {
+      const uint32_t p = P.posA(w, r);
+      z[r] = zc[P.regB(p)] || !need[p];
+    }
+    for (const Layer &L : P.fft) {
+      if (!P.inA(L.bit)) continue;
+      for (const Bf &b : L.bf) {
+        if (P.waveA(b.x) != w) continue;
+        const uint32_t rx = P.regA(b.x), ry = P.regA(b.y);
+        g.butterfly(wname(rx), z[rx], wname(ry), z[ry], false, P.get_tw(b.log_m));
+      }
+    }
+    // basis change back, planes -> bytes, store (or rec ^ parity)
+    g.ops = &g.st->ops_io;
+    for (uint32_t r = 0; r < 8; r++) {
+      const uint32_t p = P.posA(w, r);
+      if (P.out_mode[p] == kOutNone) continue;
+      const auto W = Gen::regs(wname(r));
+      if (z[r])
+        for (int i = 0; i < 8; i++) o << "  " << W[i] << " = 0u;\n";
+      else
+        g.basis_change(W);
+      o << "  { u32 Q[8] = {";
+      for (int i = 0; i < 8; i++) o << W[i] << (i < 7 ? ", " : "};\n");
+      o << "    v4 a, b; unplanes2(Q, a, b);\n";
+      g.op(4 + 48);
+      o << "    const u32 so = " << p << "u * sbl;\n";
+      if (P.out_mode[p] == kOutXorRec) o << "    a ^= LDB(RR, uo, so); b ^= LDB(RR, uo1, so);\n";
+      o << "    STB(a, RO, uo, so); STB(b, RO, uo1, so); }\n";
+    }
+    g.ops = &g.st->ops_a;
+    o << "  }\n";
+  }
+  o << "  stripe = stripe_n; uu = uu_n;\n";
+  o << "  }\n}\n";
+  return o.str();
+}
+
+}  // namespace
+
+bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
+  if (!basis().ok || m < 17 || m > 64 || k == 0) return false;
+  const uint64_t C = ceil_pow2(m);
+  if (C != 32 && C != 64) return false;
+  // high rate (root.zig:397-415) with this chunk
+  const uint64_t pk = ceil_pow2(k);
+  if (!(pk > C || (pk == C && k <= m))) return false;
+  if ((k + C - 1) / C > kMaxChunks) return false;
+  if (shard_bytes == 0 || shard_bytes % kUnitBytes) return false;
+  return k * shard_bytes + 4096 < 0x80000000ull && m * shard_bytes + 4096 < 0x80000000ull;
+}
+
+std::string cache_key(const Spec &s) {
+  // code-shape knobs are part of the key (read when the source is generated)
+  std::string k = "fft:p" + std::to_string(prefetch_of(s)) + "n" + std::to_string(nt_of()) + "s" +
+                  std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 0)) +
+                  "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + ":" + std::to_string(s.k) + ":" +
+                  std::to_string(s.m) + ":" + std::to_string(s.flags) + ":";
+  for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
+  k.push_back(':');
+  for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));
+  return k;
+}
+
+std::string kernel_name(const Spec &s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : cache_key(s)) h = (h ^ c) * 1099511628211ull;
+  char name[96];
+  std::snprintf(name, sizeof name, "rs_fft_encode_k%u_m%u_%016llx", s.k, s.m, static_cast<unsigned long long>(h));
+  return name;
+}
+
+std::string generate(const Spec &s, const std::string &name) { return gen_source(s, name, nullptr); }
+
+Stats stats(const Spec &s) {
+  Stats st;
+  (void)gen_source(s, "x", &st);
+  return st;
+}
+
+const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pending) {
+  Spec copy = s;
+  copy.prefetch = prefetch_of(s);
+  for (;;) {
+    const std::string name = kernel_name(copy);
+    const jit::Kernel *k =
+        jit::get_source(cache_key(copy), name, [copy, name] { return generate(copy, name); }, async, err, pending);
+    if (!k) return nullptr;
+    int local = 0;
+    if (hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k->fn) != hipSuccess) local = 0;
+    if (local == 0 || copy.prefetch == 0) {
+      if (local) {
+        err = "FFT kernel spills registers even without prefetch";
+        return nullptr;
+      }
+      return k;
+    }
+    copy.prefetch = copy.prefetch > 2 ? 2 : 0;  // spilled: less prefetch (fewer live registers)
+  }
+}
+
+bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_bytes) {
+  const std::string name = kernel_name(s);
+  const std::string src = generate(s, name);
+  if (const char *dir = std::getenv("RS_AMD_JIT_DUMP")) {
+    if (FILE *f = std::fopen((std::string(dir) + "/" + name + ".hip").c_str(), "w")) {
+      std::fputs(src.c_str(), f);
+      std::fclose(f);
+    }
+  }
+  return jit::compile_source_check(src, err, ms, code_bytes);
+}
+
+hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
+                  uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st) {
+  if (n_stripes == 0) return hipSuccess;
+  if (!supports(s.k, s.m, sb)) return hipErrorInvalidValue;
+  const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  int dev = 0, n_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return hipErrorInvalidDevice;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cus.find(dev);
+    if (it == cus.end()) {
+      hipError_t e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (e != hipSuccess) return e;
+      cus[dev] = n_cu;
+    } else {
+      n_cu = it->second;
+    }
+  }
+  uint32_t ups = static_cast<uint32_t>(sb / kUnitBytes);
+  uint64_t n_units = n_stripes * ups;
+  // one workgroup per CU (128 KiB of LDS for chunk 64), persistent over the units
+  const uint32_t per_cu = C == 64 ? 1 : 2;
+  const uint64_t grid = std::min<uint64_t>(n_units, static_cast<uint64_t>(n_cu) * per_cu);
+  uint32_t sb32 = static_cast<uint32_t>(sb);
+  const unsigned char *d = data, *r = rec ? rec : data;
+  unsigned char *o = out;
+  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units};
+  return hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(grid), 1, 1, (C / 8) * 64, 1, 1, 0, st, args, nullptr);
+}
+
+uint64_t selftest(const Spec &s, int trials) {
+  Plan P = make_plan(s);
+  std::mt19937_64 rng(12345);
+  uint64_t bad = 0;
+  const uint32_t C = P.C;
+  auto apply = [&](std::vector<uint16_t> &v, const Layer &L) {
+    for (const Bf &b : L.bf) {
+      const Tw &t = P.get_tw(b.log_m);
+      auto mulv = [&](uint16_t y) -> uint16_t {  // (u|v) coordinates through the kernel's blocks
+        if (t.zero) return 0;
+        uint16_t r = 0;
+        for (int i = 0; i < 8; i++) {
+          const uint8_t u = y & 0xFF, vv = y >> 8;
+          const int lo = __builtin_popcount(t.A[i] & u) ^ __builtin_popcount(t.B[i] & vv);
+          const int hi = __builtin_popcount(t.Cm[i] & u) ^ __builtin_popcount(t.D[i] & vv);
+          r |= static_cast<uint16_t>((lo & 1) << i);
+          r |= static_cast<uint16_t>((hi & 1) << (8 + i));
+        }
+        return r;
+      };
+      uint16_t &x = v[b.x], &y = v[b.y];
+      if (L.inv) {
+        y ^= x;
+        x ^= mulv(y);
+      } else {
+        x ^= mulv(y);
+        y ^= x;
+      }
+    }
+  };
+  for (int tr = 0; tr < trials; tr++) {
+    std::vector<uint16_t> in(s.k);
+    for (auto &x : in) x = static_cast<uint16_t>(rng());
+    std::vector<uint16_t> ref(s.m), in_ref = in;
+    for (uint32_t i = 0; i < s.k; i++)
+      if (i < s.skip.size() && s.skip[i]) in_ref[i] = 0;
+    scalar_encode(in_ref.data(), s.k, s.m, P.d1, (s.flags & RS_FLAG_QUIRK_D2) != 0, ref.data());
+    std::vector<uint16_t> acc(C, 0);
+    for (size_t j = 0; j < P.truncs.size(); j++) {
+      std::vector<uint16_t> v(C, 0);
+      for (uint32_t q = 0; q < C; q++) v[q] = P.valid[j][q] ? to_uv(in[j * C + q]) : 0;
+      for (const Layer &L : P.ifft[j]) apply(v, L);
+      for (uint32_t q = 0; q < C; q++) acc[q] ^= v[q];
+    }
+    for (const Layer &L : P.fft) apply(acc, L);
+    for (uint32_t q = 0; q < s.m; q++) bad += to_uv(acc[q]) != ref[q];
+  }
+  return bad;
+}
+
+}  // namespace fftnet
+}  // namespace rs

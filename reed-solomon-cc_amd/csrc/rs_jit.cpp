@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -500,9 +501,7 @@ bool enabled() {
 namespace {
 
 // source -> loaded module; no lock held (compiles run concurrently)
-std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const Tuning &tu, std::string &err) {
-  const std::string name = kernel_name(spec, key);
-  const std::string src = generate_with(spec, name, tu);
+std::unique_ptr<Kernel> build_source(const std::string &name, const std::string &src, std::string &err) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
   if (!compile(src, code, err)) return nullptr;
@@ -517,16 +516,23 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const
     err = std::string("hipModuleGetFunction: ") + hipGetErrorString(e);
     return nullptr;
   }
-  k->n_in = spec.n_in;
-  k->n_out = spec.n_out;
-  k->n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
-  k->units = static_cast<uint32_t>(tu.units);
-  k->pieces = spec.pieces;
   k->name = name;
   k->compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (std::getenv("RS_AMD_JIT_VERBOSE"))
     std::fprintf(stderr, "[rs_amd jit] %s compiled in %.0f ms (%zu B source, %zu B code)\n", name.c_str(),
                  k->compile_ms, src.size(), code.size());
+  return k;
+}
+
+std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const Tuning &tu, std::string &err) {
+  const std::string name = kernel_name(spec, key);
+  std::unique_ptr<Kernel> k = build_source(name, generate_with(spec, name, tu), err);
+  if (!k) return nullptr;
+  k->n_in = spec.n_in;
+  k->n_out = spec.n_out;
+  k->n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
+  k->units = static_cast<uint32_t>(tu.units);
+  k->pieces = spec.pieces;
   return k;
 }
 
@@ -542,10 +548,10 @@ const Kernel *insert(const std::string &key, std::unique_ptr<Kernel> k) {  // g_
 // queue and finishes only the compile in flight; it is defined after the caches
 // above, so it is destroyed (joined) before them.
 struct Job {
-  NetSpec spec;
-  std::string key;
+  std::string key, name;
+  std::function<std::string()> gen;  // the kernel source (generated on the worker)
+  std::function<void(Kernel &)> fill;  // launch metadata of the built kernel
   int dev;
-  Tuning tu;
 };
 
 struct Worker {
@@ -571,8 +577,12 @@ struct Worker {
       }
       std::string e;
       std::unique_ptr<Kernel> k;
-      if (hipSetDevice(j.dev) == hipSuccess) k = build(j.spec, j.key, j.tu, e);
-      else e = "hipSetDevice failed";
+      if (hipSetDevice(j.dev) == hipSuccess) {
+        k = build_source(j.name, j.gen(), e);
+        if (k && j.fill) j.fill(*k);
+      } else {
+        e = "hipSetDevice failed";
+      }
       std::lock_guard<std::mutex> lk(g_mu);
       if (k) insert(j.key, std::move(k));
       else g_failed.emplace(j.key, e);
@@ -652,7 +662,16 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
   if (g_pending.count(key)) return nullptr;
   g_pending.insert(key);
   try {
-    g_worker.push(Job{spec, key, dev, tu});
+    const std::string name = kernel_name(spec, key);
+    g_worker.push(Job{key, name, [spec, name, tu] { return generate_with(spec, name, tu); },
+                      [spec, tu](Kernel &k) {
+                        k.n_in = spec.n_in;
+                        k.n_out = spec.n_out;
+                        k.n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
+                        k.units = static_cast<uint32_t>(tu.units);
+                        k.pieces = spec.pieces;
+                      },
+                      dev});
   } catch (const std::exception &ex) {  // no worker thread: the table kernel stays in use
     g_pending.erase(key);
     g_failed.emplace(key, std::string("background compile unavailable: ") + ex.what());
@@ -660,6 +679,57 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
     pending = false;
   }
   return nullptr;
+}
+
+const Kernel *get_source(const std::string &key, const std::string &name, const std::function<std::string()> &gen,
+                         bool async, std::string &err, bool &pending) {
+  pending = false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    err = "hipGetDevice failed";
+    return nullptr;
+  }
+  const std::string full = std::to_string(dev) + ":src:" + key;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(full);
+    if (it != g_cache.end()) return it->second.get();
+    auto f = g_failed.find(full);
+    if (f != g_failed.end()) {
+      err = f->second;
+      return nullptr;
+    }
+    if (async && !env_on("RS_AMD_JIT_SYNC")) {
+      pending = true;
+      if (g_pending.count(full)) return nullptr;
+      g_pending.insert(full);
+      try {
+        g_worker.push(Job{full, name, gen, nullptr, dev});
+      } catch (const std::exception &ex) {
+        g_pending.erase(full);
+        g_failed.emplace(full, std::string("background compile unavailable: ") + ex.what());
+        err = g_failed[full];
+        pending = false;
+      }
+      return nullptr;
+    }
+  }
+  std::unique_ptr<Kernel> k = build_source(name, gen(), err);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!k) {
+    g_failed.emplace(full, err);
+    return nullptr;
+  }
+  return insert(full, std::move(k));
+}
+
+bool compile_source_check(const std::string &src, std::string &err, double *ms, size_t *code_bytes) {
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<char> code;
+  const bool ok = compile(src, code, err);
+  if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (code_bytes) *code_bytes = code.size();
+  return ok;
 }
 
 void wait_pending() {

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -81,6 +82,14 @@ const Kernel *get(const NetSpec &spec, std::string &err);
 // then nullptr with pending = true (a background compile has been started), or
 // nullptr with pending = false and `err` set if the compile failed.
 const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending);
+
+// Any generated kernel: `gen` returns a complete source defining extern "C" `name`;
+// compiled once per (device, key). async: compiled on the background worker
+// (nullptr + pending until it is loaded; RS_AMD_JIT_SYNC=1 compiles in the caller).
+const Kernel *get_source(const std::string &key, const std::string &name, const std::function<std::string()> &gen,
+                         bool async, std::string &err, bool &pending);
+// hipRTC compile of a source only (no device): a build check.
+bool compile_source_check(const std::string &src, std::string &err, double *ms, size_t *code_bytes);
 
 // Block until no background compile is running (rs_net_wait).
 void wait_pending();
