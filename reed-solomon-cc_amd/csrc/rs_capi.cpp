@@ -137,6 +137,7 @@ uint32_t async_after() {
 struct FftSlot {
   std::mutex mu;
   bool failed = false;
+  bool async = false;  // per-pattern kernels: background compile, the table encode meanwhile
   fftnet::Spec spec;
 };
 
@@ -151,7 +152,8 @@ const jit::Kernel *fft_kernel(FftSlot &slot) {
   std::string err;
   bool pending = false;
   const char *a = std::getenv("RS_AMD_FFT_ASYNC");
-  const jit::Kernel *k = fftnet::get(slot.spec, a && *a && std::strcmp(a, "0") != 0, err, pending);
+  const bool async = a && *a ? std::strcmp(a, "0") != 0 : slot.async;
+  const jit::Kernel *k = fftnet::get(slot.spec, async, err, pending);
   if (!k && !pending) {
     slot.failed = true;
     std::fprintf(stderr, "[rs_amd] bit-sliced FFT kernel unavailable, using table kernels: %s\n", err.c_str());
@@ -177,6 +179,7 @@ struct DecodePlan {
   // a scratch, then the e x e matrix kernel on rec ^ scratch rows (see syndrome_map)
   bool syndrome = false;
   std::shared_ptr<DevBuf> skip;  // k-bit mask of the erased data shards
+  std::shared_ptr<FftSlot> syn_fft;  // the syndromes' encode on the bit-sliced FFT kernel (wide codes)
 };
 
 // Compile (once) and return the plan's network kernel; nullptr if hipRTC failed
@@ -484,6 +487,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
                     std::to_string(jit::enabled() && jit::shard_ok(sb)) + "/" +
+                    std::to_string(fft_enabled() && fftnet::supports(k, m, sb)) + "/" +
                     std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
@@ -530,6 +534,19 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
         if (!present[i]) bits[i / 32] |= 1u << (i % 32);
       if ((st = upload(bits.data(), bits.size() * sizeof(uint32_t), dev, plan->skip))) return st;
       plan->syndrome = true;
+      if (fft_enabled() && fftnet::supports(k, m, sb)) {
+        // Enc(d') on the FFT kernel: erased data shards read as zero, only the rows R stored
+        plan->syn_fft = std::make_shared<FftSlot>();
+        plan->syn_fft->async = true;
+        fftnet::Spec &fs = plan->syn_fft->spec;
+        fs.k = static_cast<uint32_t>(k);
+        fs.m = static_cast<uint32_t>(m);
+        fs.flags = RS_FLAG_CORRECTED;
+        fs.skip.assign(k, 0);
+        for (uint64_t i = 0; i < k; i++) fs.skip[i] = present[i] ? 0 : 1;
+        fs.out_mode.assign(m, fftnet::kOutNone);
+        for (int32_t src : map.src) fs.out_mode[src & kSrcIndexMask] = fftnet::kOutStore;
+      }
     } else {
       reconstruct_map(k, m, flags, present, map);
     }
@@ -977,7 +994,9 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
     return net_name("reconstruct", k, e);
   if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
     thread_local std::string name;
-    name = std::string("syndrome+") + choose_encode(k, m, sb, 4).name + "+";
+    name = std::string("syndrome+") +
+           (fft_enabled() && fftnet::supports(k, m, sb) ? net_name("fft_encode", k, m) : choose_encode(k, m, sb, 4).name) +
+           "+";
     if (jit::enabled() && jit::supports_async(static_cast<uint32_t>(e), static_cast<uint32_t>(e), sb))
       name += net_name("syndrome", e, e);
     else
@@ -1276,7 +1295,12 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
         db.xsrc = static_cast<const uint8_t *>(scratch);
         db.xsrc_stripe_stride = m * sb;
         db.n_stripes = cnt;
-        hipError_t err = launch_encode(ke, eb, s);
+        hipError_t err = hipSuccess;
+        const jit::Kernel *fk = plan->syn_fft && max_nv == 4 ? fft_kernel(*plan->syn_fft) : nullptr;
+        if (fk)
+          err = fftnet::launch(*fk, plan->syn_fft->spec, eb.data, orig_stride, nullptr, 0, eb.parity, m * sb, sb, cnt, s);
+        else
+          err = launch_encode(ke, eb, s);
         if (err == hipSuccess) {
           if (nk)
             err = jit::launch(*nk, db.orig, orig_stride, db.rec, rec_stride, db.out, out_stride, sb, cnt, s, db.xsrc,

@@ -271,7 +271,7 @@ int env_int(const char *name, int def) {
   return e && *e ? std::atoi(e) : def;
 }
 
-int nt_of() { return env_int("RS_AMD_FFT_NT", 0) & 3; }
+int nt_of() { return env_int("RS_AMD_FFT_NT", 3) & 3; }
 
 int prefetch_of(const Spec &s) {
   return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", 4)));
@@ -506,7 +506,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   const uint32_t NW = P.NW, C = P.C;
   bool any_xor = false;
   for (uint32_t q = 0; q < s.m; q++) any_xor |= P.out_mode[q] == kOutXorRec;
-  // RS_AMD_FFT_NT: non-temporal loads (bit 0) / stores (bit 1) (cache policy bit nt = 2)
+  // RS_AMD_FFT_NT: non-temporal loads (bit 0) / stores (bit 1) (cache policy bit nt = 2);
+  // default both: RS(200,55) 256 KiB encode 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
   const int nt = nt_of();
   o << "#define RS_AUX_LD " << ((nt & 1) ? 2 : 0) << "\n#define RS_AUX_ST " << ((nt & 2) ? 2 : 0) << "\n" << kPrelude;
   o << "extern \"C\" __global__ __launch_bounds__(" << NW * 64 << ") void " << name
@@ -548,8 +549,9 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     for (int i = 0; i < 8; i++) hdr2 << "w" << r << "_" << i << ", b" << r << "_" << i << ", c" << r << "_" << i << (r == 7 && i == 7 ? ";\n" : ", ");
 
   // LDS slot accesses (RS_AMD_FFT_LDS128: 4-dword accesses, planes 4q..4q+3 of a slot
-  // in quad q; else dword accesses, plane i at (s * 8 + i) * 64)
-  const bool l128 = env_int("RS_AMD_FFT_LDS128", 0) != 0;
+  // in quad q — the default, 3.77 -> 3.54 ms on RS(200,55) in spite of 17 more VGPRs for
+  // the 4-register tuples; else dword accesses, plane i at (s * 8 + i) * 64)
+  const bool l128 = env_int("RS_AMD_FFT_LDS128", 1) != 0;
   auto lds_write = [&](const std::string &wexpr, uint32_t slot, const std::vector<std::string> &v) {
     // slot address = wexpr (runtime, in slots) + slot
     for (int q = 0; q < (l128 ? 2 : 8); q++) {
@@ -820,7 +822,7 @@ bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft:p" + std::to_string(prefetch_of(s)) + "n" + std::to_string(nt_of()) + "s" +
-                  std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 0)) +
+                  std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 1)) +
                   "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + ":" + std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":";
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));

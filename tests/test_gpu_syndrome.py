@@ -102,9 +102,32 @@ def test_syndrome_network_background_compile(oracle, monkeypatch):
     lost = sorted(int(i) for i in rng.choice(k, size=55, replace=False))
     present = np.ones(k + m, np.uint8)
     present[lost] = 0
-    assert R.reconstruct_kernel_name(k, m, sb, present) == "syndrome+encode_ws64_nv1+net_syndrome_i55_o55"
+    assert R.reconstruct_kernel_name(k, m, sb, present) == "syndrome+net_fft_encode_i200_o55+net_syndrome_i55_o55"
     for _ in range(2):  # 2nd use queues the compile (RS_AMD_NET_ASYNC_AFTER)
         assert (reconstruct(k, m, present, data, par) == data[:, lost]).all()
     R.net_wait()
     assert (reconstruct(k, m, present, data, par) == data[:, lost]).all()
 
+
+
+@pytest.mark.parametrize("k,m", [(200, 55), (70, 33), (64, 64), (100, 20), (300, 40)])
+def test_syndrome_fft_encode_vs_oracle(oracle, monkeypatch, k, m):
+    """The syndromes' encode on the bit-sliced FFT kernel (erased shards skipped, only
+    the rows R stored), compiled synchronously, then the e x e map."""
+    monkeypatch.setenv("RS_AMD_DECODE", "syndrome")
+    monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")
+    rng = np.random.default_rng(k * 31 + m)
+    sb, n = 4096, 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=8)
+    for trial in range(2):
+        e = int(rng.integers(1, min(k, m) + 1))
+        lost = list(rng.choice(k, size=e, replace=False))
+        extra = int(rng.integers(0, m - e + 1))
+        lost += [k + int(i) for i in rng.choice(m, size=extra, replace=False)]
+        present = np.ones(k + m, np.uint8)
+        present[lost] = 0
+        missing = [i for i in range(k) if not present[i]]
+        name = R.reconstruct_kernel_name(k, m, sb, present)
+        assert "fft_encode" in name, name
+        assert (reconstruct(k, m, present, data, par) == data[:, missing]).all(), (k, m, sorted(lost), name)
