@@ -44,55 +44,86 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(k, m, sb, erase, budget_s):
-    """Oracle (C restatement of the reference engine, AVX2 pshufb) on the host
-    cores: the same step (encode + reconstruct) on a bounded stripe sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-
+def _threads():
+    """Host threads for the CPU leg: the cores this process may run on, capped at the
+    GPU box's CPU share (16 per GPU: the harness sizes worker pools to it; os.cpu_count()
+    there reports the whole machine). The per-core rate is reported beside it."""
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    return max(1, min(int(os.environ.get("RS_BENCH_CPU_THREADS", "16")), cores)), cores
+
+
+def _cpu_leg(O, k, m, sb, erase, n_stripes, threads, rng):
+    """Oracle (C restatement of the reference engine, AVX2 pshufb) encode + reconstruct
+    of n_stripes stripes: (GiB/s combined, encode GiB/s, reconstruct GiB/s)."""
     present = np.ones(k + m, np.uint8)
     present[erase] = 0
+    data = rng.integers(0, 256, (n_stripes, k, sb), dtype=np.uint8)
+    t0 = time.perf_counter()
+    par = O.encode_batch(k, m, data, threads=threads)
+    t1 = time.perf_counter()
+    O.reconstruct_batch(k, m, present, np.concatenate([data, par], axis=1), threads=threads)
+    t2 = time.perf_counter()
+    gib = k * sb * n_stripes / 2**30
+    return 2 * gib / (t2 - t0), gib / (t1 - t0), gib / (t2 - t1)
+
+
+def cpu_baseline(k, m, sb, erase, budget_s):
+    """Oracle on the host cores: the same step (encode + reconstruct) on a bounded
+    stripe sample, single-threaded and on `threads` cores; plus the other BASELINE
+    configs (c0: RS(4,2) 64 KiB, benchmarks.zig:25-60 protocol; c4: RS(200,55) 256 KiB
+    losing 55 data shards) and the reference harness shapes."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    threads, cores = _threads()
     rng = np.random.default_rng(7)
-
-    def run(n_stripes, thr):
-        data = rng.integers(0, 256, (n_stripes, k, sb), dtype=np.uint8)
-        t0 = time.perf_counter()
-        par = O.encode_batch(k, m, data, threads=thr)
-        t1 = time.perf_counter()
-        O.reconstruct_batch(k, m, present, np.concatenate([data, par], axis=1), threads=thr)
-        t2 = time.perf_counter()
-        return n_stripes, t1 - t0, t2 - t1
-
     # calibrate on one stripe single-threaded, then size both legs to the budget
-    _, te, tr = run(1, 1)
-    per_stripe = te + tr
-    n1 = max(1, int(budget_s * 0.3 / per_stripe))
-    n1 = min(n1, 32)
-    s1, e1, r1 = run(n1, 1)
-    nt = max(threads, int(budget_s * 0.6 / per_stripe * threads))
-    nt = min(nt, 64)
-    st, et, rt = run(nt, threads)
-    gib = k * sb / 2**30
+    per_stripe = 2 * k * sb / 2**30 / _cpu_leg(O, k, m, sb, erase, 1, 1, rng)[0]
+    n1 = max(1, min(32, int(budget_s * 0.25 / per_stripe)))
+    v1, e1, r1 = _cpu_leg(O, k, m, sb, erase, n1, 1, rng)
+    nt = max(threads, min(64, int(budget_s * 0.45 / per_stripe * threads)))
+    vt, et, rt = _cpu_leg(O, k, m, sb, erase, nt, threads, rng)
+    # c4: RS(200,55) 256 KiB, 55 erased data shards (every third), threads stripes
+    c4_erase = list(range(1, 200, 3))[:55]
+    v4, e4, r4 = _cpu_leg(O, 200, 55, 256 << 10, c4_erase, threads, threads, rng)
     return {
-        "value": round(2 * gib * st / (et + rt), 3),
+        "value": round(vt, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"RS({k},{m}) {sb >> 10} KiB shards, {st} stripes encode + reconstruct {len(erase)} erased, "
-                  f"{threads} threads (oracle/rs_oracle.c AVX2 engine)",
-        "single_thread": {"value": round(2 * gib * s1 / (e1 + r1), 3), "cores": 1,
-                          "encode_GiBps": round(gib * s1 / e1, 3), "reconstruct_GiBps": round(gib * s1 / r1, 3),
-                          "sample_stripes": s1},
-        "encode_GiBps": round(gib * st / et, 3),
-        "reconstruct_GiBps": round(gib * st / rt, 3),
+        "sample": f"RS({k},{m}) {sb >> 10} KiB shards, {nt} stripes encode + reconstruct {len(erase)} erased, "
+                  f"{threads} threads of {cores} visible (oracle/rs_oracle.c AVX2 engine)",
+        "single_thread": {"value": round(v1, 3), "cores": 1, "encode_GiBps": round(e1, 3),
+                          "reconstruct_GiBps": round(r1, 3), "sample_stripes": n1},
+        "per_core_GiBps": round(vt / threads, 3),
+        "encode_GiBps": round(et, 3),
+        "reconstruct_GiBps": round(rt, 3),
+        "per_config": {
+            "c0 RS(4,2) 64KiB 1 stripe insert+encode us (benchmarks.zig protocol, 1 thread)":
+                round(O.bench_encode_ns(4, 2, 64 << 10, 500) / 1e3, 3),
+            "c1/c2 RS(10,4) 1MiB encode+reconstruct4 GiB/s": round(vt, 3),
+            "c4 RS(200,55) 256KiB encode GiB/s": round(e4, 3),
+            "c4 RS(200,55) 256KiB reconstruct55 GiB/s": round(r4, 3),
+            "c4 sample": f"{threads} stripes, {threads} threads",
+        },
         "harness": harness_protocol(O),
         "cpu_model": _cpu_model(),
     }
+
+
+def verify_parity(k, m, data, parity, stripes=(0, -1)):
+    """Checker, outside the timed region: the GPU parity of a few whole stripes against
+    the oracle (C restatement of the reference, oracle/rs_oracle.c)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    idx = sorted({s % data.shape[0] for s in stripes})
+    d = data[idx].cpu().numpy()
+    got = parity[idx].cpu().numpy()
+    return bool((O.encode_batch(k, m, d, threads=_threads()[0]) == got).all())
 
 
 def harness_protocol(O, iters=2000):
@@ -183,8 +214,8 @@ def main():
     rec_ms = max_over_ranks(rec_ms, device=dev)
 
     ok = None
-    if not args.no_verify:
-        ok = all_ok(bool(torch.equal(restored, data[:, erase])), device=dev)
+    if not args.no_verify:  # restored == erased data, and 2 whole stripes' parity == the oracle's
+        ok = all_ok(bool(torch.equal(restored, data[:, erase])) and verify_parity(k, m, data, parity), device=dev)
 
     if rank == 0:
         data_bytes = k * sb * n  # per rank per op
@@ -202,7 +233,9 @@ def main():
                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
                     # HBM bytes per launch from PMC (profiles/traffic.json, per stripe x this batch)
                     "traffic": int(tr["hbm_bytes_per_stripe"] * n) if tr else None,
-                    "traffic_source": tr["method"] + "; " + tr["workload"] if tr else None,
+                    "traffic_source": (tr["method"] + "; " + tr["workload"] +
+                                       ("" if tr.get("stripes_per_launch") == n else
+                                        f"; scaled per stripe to {n} stripes")) if tr else None,
                     "kernel": kname, "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ms, 4),
                     "per_kernel": {kk: {"kernel": v[2], "avg_ms": round(v[0], 4),
                                         "achieved_GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 1),
@@ -215,6 +248,9 @@ def main():
         out = {
             "metric": "device-resident encode+reconstruct GiB/s per GPU (RS(10,4), 1 MiB shards); % HBM roofline",
             "value": round(gib, 2),
+            "value_per_gpu": round(gib / world, 2),
+            "value_note": "value = user data encoded + reconstructed by all GPUs per second (whole job); "
+                          "value_per_gpu = value / n_gpus",
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -234,6 +270,7 @@ def main():
             "encode_GiBps": round(data_bytes * world / (enc_ms * 1e-3) / 2**30, 2),
             "reconstruct_GiBps": round(data_bytes * world / (rec_ms * 1e-3) / 2**30, 2),
             "verified": ok,
+            "verified_how": "restored shards == erased data on every stripe; parity of stripes 0 and n-1 == oracle",
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -176,6 +176,11 @@ const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recover
  * RS_AMD_JIT_SYNC=1 compiles them in the calling thread instead. Returns RS_OK. */
 int rs_net_wait(void);
 
+/* hipRTC activity of this process: kernels compiled, code objects found in the on-disk
+ * cache ($RS_AMD_CACHE_DIR, else $XDG_CACHE_HOME/rs_amd or ~/.cache/rs_amd; empty = off),
+ * modules loaded. Any pointer may be NULL. */
+int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules);
+
 /* Plan-time network kernel: generate the bit-sliced network of an encode (present
  * == NULL) or of one reconstruct pattern and compile it with hipRTC for gfx950, without
  * loading it (no device needed: a build check). *compile_ms (optional) = compile time.

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -122,7 +123,7 @@ struct DevBuf {
 // Bit-sliced network kernel of a plan (rs_jit.hpp), compiled on first use.
 struct NetSlot {
   std::mutex mu;
-  bool failed = false;
+  bool failed[3] = {false, false, false};  // per variant: 4 KiB units, 2 / 4 stripes per unit (small shards)
   bool async = false;  // past the synchronous size cap: compiled in the background
   uint32_t uses = 0;   // async: the compile starts at the RS_AMD_NET_ASYNC_AFTER-th use (default 2)
   jit::NetSpec spec;
@@ -131,6 +132,24 @@ struct NetSlot {
 uint32_t async_after() {
   const char *e = std::getenv("RS_AMD_NET_ASYNC_AFTER");
   return e && *e ? static_cast<uint32_t>(std::max(1, std::atoi(e))) : 2u;
+}
+
+// Encodes of 1 / 2 KiB shards stay on the table kernels, which measured as fast or
+// faster there (RS(10,4) 2 KiB 0.644 vs 0.678 ms, RS(4,2) 1 KiB 0.528 vs 0.541 ms,
+// profiles/r01/sweep_small_shard_networks.jsonl); reconstructs take the networks
+// (RS(10,4) 1 KiB losing 4: 1.16 -> 0.67 ms). RS_AMD_NET_SMALL_ENCODE=1 overrides.
+bool encode_net_ok(uint64_t sb) {
+  if (jit::net_pieces(sb) == 1) return true;
+  const char *e = std::getenv("RS_AMD_NET_SMALL_ENCODE");
+  return e && *e && std::strcmp(e, "0") != 0;
+}
+
+// A fallback to the table kernels is reported on stderr once per distinct reason.
+void warn_once_per_reason(const char *what, const std::string &err) {
+  static std::mutex mu;
+  static std::set<std::string> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  if (seen.insert(err.substr(0, 200)).second) std::fprintf(stderr, "%s%s\n", what, err.c_str());
 }
 
 // Bit-sliced FFT kernel of a plan (rs_fftnet.hpp): wide codes, compiled on first use.
@@ -156,7 +175,7 @@ const jit::Kernel *fft_kernel(FftSlot &slot) {
   const jit::Kernel *k = fftnet::get(slot.spec, async, err, pending);
   if (!k && !pending) {
     slot.failed = true;
-    std::fprintf(stderr, "[rs_amd] bit-sliced FFT kernel unavailable, using table kernels: %s\n", err.c_str());
+    warn_once_per_reason("[rs_amd] bit-sliced FFT kernel unavailable, using table kernels: ", err);
   }
   return k;
 }
@@ -189,7 +208,9 @@ struct DecodePlan {
 // 1 / 2 KiB shards run a variant whose wave units span 4 / 2 stripes (jit::net_pieces).
 const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
   std::lock_guard<std::mutex> lk(slot.mu);
-  if (slot.failed) return nullptr;
+  const uint32_t pieces = jit::net_pieces(sb);
+  const int vi = pieces >= 4 ? 2 : pieces >= 2 ? 1 : 0;  // a failed variant does not disable the others
+  if (slot.failed[vi]) return nullptr;
   std::string err;
   bool pending = false;
   if (slot.async && slot.uses < async_after()) {  // a one-off pattern is not worth a background compile
@@ -197,7 +218,6 @@ const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
     if (!(sync && *sync && std::strcmp(sync, "0") != 0) && ++slot.uses < async_after()) return nullptr;
   }
   jit::NetSpec small;
-  const uint32_t pieces = jit::net_pieces(sb);
   if (pieces > 1) {
     small = slot.spec;
     small.pieces = pieces;
@@ -205,15 +225,55 @@ const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
   const jit::NetSpec &spec = pieces > 1 ? small : slot.spec;
   const jit::Kernel *k = slot.async ? jit::get_async(spec, err, pending) : jit::get(spec, err);
   if (!k && !pending) {
-    slot.failed = true;
-    std::fprintf(stderr, "[rs_amd] bit-sliced network unavailable, using table kernels: %s\n", err.c_str());
+    slot.failed[vi] = true;
+    warn_once_per_reason("[rs_amd] bit-sliced network unavailable, using table kernels: ", err);
   }
   return k;
 }
 
+// Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
+// kind) are dropped (a plan in use stays alive through its shared_ptr). g_plan_mu
+// guards the maps only: plans are built without it (double-checked insertion; two
+// threads racing on a new key may both build, the first insert wins).
+size_t plan_cache_cap() {
+  const char *e = std::getenv("RS_AMD_PLAN_CACHE");
+  return e && *e ? static_cast<size_t>(std::max(1, std::atoi(e))) : 4096u;
+}
+
+template <class V>
+struct PlanCache {
+  std::map<std::string, std::pair<std::shared_ptr<V>, uint64_t>> m;  // plan, last use
+  uint64_t tick = 0;
+  std::shared_ptr<V> find(const std::string &k) {  // g_plan_mu held
+    auto it = m.find(k);
+    if (it == m.end()) return nullptr;
+    it->second.second = ++tick;
+    return it->second.first;
+  }
+  std::shared_ptr<V> insert(const std::string &k, std::shared_ptr<V> v) {  // g_plan_mu held
+    auto it = m.find(k);
+    if (it != m.end()) {
+      it->second.second = ++tick;
+      return it->second.first;
+    }
+    const size_t cap = plan_cache_cap();
+    if (m.size() >= cap) {  // drop the oldest eighth (amortised O(1) per insert)
+      std::vector<std::pair<uint64_t, std::string>> age;
+      age.reserve(m.size());
+      for (auto &kv : m) age.emplace_back(kv.second.second, kv.first);
+      const size_t drop = std::max<size_t>(1, m.size() - cap + cap / 8);
+      std::nth_element(age.begin(), age.begin() + (drop - 1), age.end());
+      for (size_t i = 0; i < drop; i++) m.erase(age[i].second);
+    }
+    m.emplace(k, std::make_pair(v, ++tick));
+    return v;
+  }
+  size_t size() const { return m.size(); }
+};
+
 std::mutex g_plan_mu;
-std::map<std::string, std::shared_ptr<EncodePlan>> g_enc_plans;
-std::map<std::string, std::shared_ptr<DecodePlan>> g_dec_plans;
+PlanCache<EncodePlan> g_enc_plans;
+PlanCache<DecodePlan> g_dec_plans;
 
 int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out) {
   auto b = std::make_shared<DevBuf>();
@@ -296,11 +356,9 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu/%llu", dev, (unsigned long long)k, (unsigned long long)m,
                 flags, static_cast<unsigned long long>(jit::max_blocks()),
                 static_cast<unsigned long long>(jit::max_async_blocks()));
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto it = g_enc_plans.find(key);
-  if (it != g_enc_plans.end()) {
-    out = it->second;
-    return RS_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if ((out = g_enc_plans.find(key))) return RS_OK;
   }
   const bool d1 = flags & RS_FLAG_QUIRK_D1, d2 = flags & RS_FLAG_QUIRK_D2;
   const uint64_t C = ceil_pow2(m);
@@ -326,8 +384,8 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
     plan->fft->spec.m = static_cast<uint32_t>(m);
     plan->fft->spec.flags = flags;
   }
-  g_enc_plans.emplace(key, plan);
-  out = plan;
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_enc_plans.insert(key, plan);
   return RS_OK;
 }
 
@@ -491,11 +549,9 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
                     std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto it = g_dec_plans.find(key);
-  if (it != g_dec_plans.end()) {
-    out = it->second;
-    return RS_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if ((out = g_dec_plans.find(key))) return RS_OK;
   }
   const bool d1 = flags & RS_FLAG_QUIRK_D1;
   const uint64_t C = ceil_pow2(m), end = C + k, W = ceil_pow2(C + k);
@@ -574,8 +630,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     plan->n_in = static_cast<uint32_t>(n_in);
     plan->off_mat = 0;
     plan->off_src = tabs.size() * sizeof(RsTab);
-    g_dec_plans.emplace(key, plan);
-    out = plan;
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    out = g_dec_plans.insert(key, plan);
     return RS_OK;
   }
 
@@ -621,8 +677,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   plan->off_post = plan->off_pre + W * sizeof(RsTab);
   plan->off_src = off_src;
   plan->off_dst = off_dst;
-  g_dec_plans.emplace(key, plan);
-  out = plan;
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_dec_plans.insert(key, plan);
   return RS_OK;
 }
 
@@ -718,7 +774,7 @@ struct MapPlan {
   size_t off_src = 0;
   std::shared_ptr<NetSlot> net;
 };
-std::map<std::string, std::shared_ptr<MapPlan>> g_map_plans;
+PlanCache<MapPlan> g_map_plans;
 
 int build_map_plan(int dev, jit::NetSpec &&spec, std::shared_ptr<MapPlan> &out) {
   auto p = std::make_shared<MapPlan>();
@@ -785,17 +841,16 @@ int run_map(const MapPlan &p, uint64_t sb, uint64_t n, const uint8_t *b0, uint64
 int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<MapPlan> &out) {
   const std::string key = "lowenc/" + std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                           std::to_string(flags & RS_FLAG_QUIRK_D1);
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto it = g_map_plans.find(key);
-  if (it != g_map_plans.end()) {
-    out = it->second;
-    return RS_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if ((out = g_map_plans.find(key))) return RS_OK;
   }
   jit::NetSpec spec;
   encode_low_map(k, m, flags, spec);
   int st = build_map_plan(dev, std::move(spec), out);
   if (st) return st;
-  g_map_plans.emplace(key, out);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_map_plans.insert(key, out);
   return RS_OK;
 }
 
@@ -810,17 +865,16 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const u
   std::string key = "lowdec/" + std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags & RS_FLAG_QUIRK_D1) + "/";
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto it = g_map_plans.find(key);
-  if (it != g_map_plans.end()) {
-    out = it->second;
-    return RS_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if ((out = g_map_plans.find(key))) return RS_OK;
   }
   jit::NetSpec spec;
   int st = low_decode_map(k, m, flags, present, spec);
   if (st) return st;
   if ((st = build_map_plan(dev, std::move(spec), out))) return st;
-  g_map_plans.emplace(key, out);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_map_plans.insert(key, out);
   return RS_OK;
 }
 
@@ -968,7 +1022,8 @@ const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
     return "lowrate_matrix";
   }
   if (fft_enabled() && fftnet::supports(k, m, sb)) return net_name("fft_encode", k, m);
-  if (jit::enabled() && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) return net_name("encode", k, m);
+  if (jit::enabled() && encode_net_ok(sb) && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))
+    return net_name("encode", k, m);
   return choose_encode(k, m, sb, 4).name;
 }
 const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const uint8_t *present) {
@@ -1009,6 +1064,13 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
     case 2: return choose_decode_mtile(static_cast<uint32_t>(e), sb, 4).name;
     default: return choose_decode(k, m, sb, 4).name;
   }
+}
+
+int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules) {
+  return guarded([&]() -> int {
+    jit::compile_stats(compiles, cache_hits, modules);
+    return RS_OK;
+  });
 }
 
 int rs_net_wait(void) {
@@ -1127,7 +1189,7 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
         return RS_OK;
       }
     }
-    if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in &&
+    if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in && encode_net_ok(sb) &&
         jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
       if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
@@ -1619,6 +1681,20 @@ uint64_t host_slice_bytes() {
   return (e && *e ? static_cast<uint64_t>(std::max(1, std::atoi(e))) : 256ull) << 20;
 }
 
+// Every slot stream is drained before a host-batch call returns, also after an error:
+// no copy into the caller's buffers (or out of them) outlives the call.
+int drain_after(Pipeline &p, int rc) {
+  const int fin = p.finish();
+  return rc ? rc : fin;
+}
+
+// Fault injection for the error-path test (the reference's checkAllAllocationFailures,
+// tests.zig:131-156, in spirit): RS_AMD_INJECT_HOST_FAIL=i fails slice i of a host batch.
+bool inject_host_failure(uint64_t slice) {
+  const char *e = std::getenv("RS_AMD_INJECT_HOST_FAIL");
+  return e && *e && std::strtoull(e, nullptr, 10) == slice;
+}
+
 // process-lifetime rings (never freed: the HIP runtime reclaims them at exit)
 std::mutex g_pipe_mu;
 std::map<int, Pipeline *> g_pipes;
@@ -1653,17 +1729,22 @@ int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const vo
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
     if ((st = p.ensure(bytes, slots))) return st;
-    for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
-      const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
-      const uint64_t cnt = std::min(S, n - s0);
-      hipStream_t q = p.st[slot];
-      HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride, orig_stride,
-                        k * sb, cnt, hipMemcpyHostToDevice, q));
-      if ((st = rs_encode_batch_dev(k, m, sb, cnt, p.buf[slot][0], 0, p.buf[slot][1], 0, flags, q))) return st;
-      HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb, m * sb,
-                        cnt, hipMemcpyDeviceToHost, q));
-    }
-    return p.finish();
+    auto slices = [&]() -> int {
+      for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
+        const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
+        const uint64_t cnt = std::min(S, n - s0);
+        hipStream_t q = p.st[slot];
+        if (inject_host_failure(i)) return fail(RS_ERR_DEVICE, "injected host-batch failure");
+        HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride,
+                          orig_stride, k * sb, cnt, hipMemcpyHostToDevice, q));
+        int rc = rs_encode_batch_dev(k, m, sb, cnt, p.buf[slot][0], 0, p.buf[slot][1], 0, flags, q);
+        if (rc) return rc;
+        HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb,
+                          m * sb, cnt, hipMemcpyDeviceToHost, q));
+      }
+      return RS_OK;
+    };
+    return drain_after(p, slices());
   });
 }
 
@@ -1691,28 +1772,32 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
     if ((st = p.ensure(bytes, slots))) return st;
-    for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
-      const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
-      const uint64_t cnt = std::min(S, n - s0);
-      hipStream_t q = p.st[slot];
-      // only the present shards cross PCIe
-      for (uint64_t j = 0; j < k; j++)
-        if (present[j])
-          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + j * sb, k * sb,
-                            static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + j * sb, orig_stride, sb, cnt,
-                            hipMemcpyHostToDevice, q));
-      for (uint64_t j = 0; j < m; j++)
-        if (present[k + j])
-          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + j * sb, m * sb,
-                            static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + j * sb, rec_stride, sb, cnt,
-                            hipMemcpyHostToDevice, q));
-      if ((st = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
-                                         p.buf[slot][2], 0, flags, q)))
-        return st;
-      HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb, e * sb,
-                        cnt, hipMemcpyDeviceToHost, q));
-    }
-    return p.finish();
+    auto slices = [&]() -> int {
+      for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
+        const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
+        const uint64_t cnt = std::min(S, n - s0);
+        hipStream_t q = p.st[slot];
+        if (inject_host_failure(i)) return fail(RS_ERR_DEVICE, "injected host-batch failure");
+        // only the present shards cross PCIe
+        for (uint64_t j = 0; j < k; j++)
+          if (present[j])
+            HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + j * sb, k * sb,
+                              static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + j * sb, orig_stride, sb, cnt,
+                              hipMemcpyHostToDevice, q));
+        for (uint64_t j = 0; j < m; j++)
+          if (present[k + j])
+            HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + j * sb, m * sb,
+                              static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + j * sb, rec_stride, sb, cnt,
+                              hipMemcpyHostToDevice, q));
+        int rc = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
+                                          p.buf[slot][2], 0, flags, q);
+        if (rc) return rc;
+        HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb,
+                          e * sb, cnt, hipMemcpyDeviceToHost, q));
+      }
+      return RS_OK;
+    };
+    return drain_after(p, slices());
   });
 }
 

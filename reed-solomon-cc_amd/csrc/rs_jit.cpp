@@ -3,6 +3,10 @@
 #include "rs_jit.hpp"
 
 #include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
 
 #include <chrono>
 #include <condition_variable>
@@ -445,15 +449,88 @@ std::string kernel_name(const NetSpec &spec, const std::string &key) {
   return name;
 }
 
-// hipRTC: source -> gfx950 code object (needs no device)
+// On-disk code-object cache: $RS_AMD_CACHE_DIR (empty = off), else
+// $XDG_CACHE_HOME/rs_amd or ~/.cache/rs_amd. An entry is named by two 64-bit hashes
+// of (hipRTC version, options, source) and its source length, so a process restart,
+// another rank or another thread finds the code object instead of recompiling.
+std::string cache_dir() {
+  if (const char *d = std::getenv("RS_AMD_CACHE_DIR")) return d;
+  if (const char *x = std::getenv("XDG_CACHE_HOME"))
+    if (*x) return std::string(x) + "/rs_amd";
+  if (const char *h = std::getenv("HOME"))
+    if (*h) return std::string(h) + "/.cache/rs_amd";
+  return "";
+}
+
+std::atomic<uint64_t> g_compiles{0}, g_disk_hits{0};
+
+std::string cache_path(const std::string &dir, const std::string &src, const char *const *opts, int n_opts) {
+  int major = 0, minor = 0;
+  hiprtcVersion(&major, &minor);
+  std::string id = "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + "\n";
+  for (int i = 0; i < n_opts; i++) id += std::string(opts[i]) + "\n";
+  id += src;
+  uint64_t h1 = 1469598103934665603ull, h2 = 0x9E3779B97F4A7C15ull;
+  for (unsigned char c : id) {
+    h1 = (h1 ^ c) * 1099511628211ull;
+    h2 = (h2 ^ c) * 0x100000001B3ull + 0x2545F4914F6CDD1Dull;
+  }
+  char name[96];
+  std::snprintf(name, sizeof name, "/%016llx%016llx-%zu.co", static_cast<unsigned long long>(h1),
+                static_cast<unsigned long long>(h2), id.size());
+  return dir + name;
+}
+
+bool cache_read(const std::string &path, std::vector<char> &code) {
+  FILE *f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  bool ok = n > 0;
+  if (ok) {
+    code.resize(static_cast<size_t>(n));
+    ok = std::fread(code.data(), 1, code.size(), f) == code.size();
+  }
+  std::fclose(f);
+  return ok;
+}
+
+void cache_write(const std::string &dir, const std::string &path, const std::vector<char> &code) {
+  std::string cur;  // mkdir -p
+  for (size_t i = 0; i <= dir.size(); i++) {
+    if (i == dir.size() || dir[i] == '/') {
+      if (!cur.empty()) ::mkdir(cur.c_str(), 0755);
+    }
+    if (i < dir.size()) cur.push_back(dir[i]);
+  }
+  char tmp_suffix[64];
+  std::snprintf(tmp_suffix, sizeof tmp_suffix, ".tmp.%d.%zu", static_cast<int>(::getpid()),
+                std::hash<std::thread::id>()(std::this_thread::get_id()));
+  const std::string tmp = path + tmp_suffix;
+  FILE *f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const bool ok = std::fwrite(code.data(), 1, code.size(), f) == code.size();
+  std::fclose(f);
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());  // atomic publish
+}
+
+// hipRTC: source -> gfx950 code object (needs no device), through the disk cache
 bool compile(const std::string &src, std::vector<char> &code, std::string &err) {
+  // -O1/-O2 measured no faster to compile (the time is in the backend)
+  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const std::string dir = cache_dir();
+  const std::string path = dir.empty() ? std::string() : cache_path(dir, src, opts, 3);
+  if (!path.empty() && cache_read(path, code)) {
+    g_disk_hits++;
+    if (std::getenv("RS_AMD_JIT_VERBOSE")) std::fprintf(stderr, "[rs_amd jit] code-object cache hit %s\n", path.c_str());
+    return true;
+  }
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "rs_net.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";
     return false;
   }
-  // -O1/-O2 measured no faster to compile (the time is in the backend)
-  const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t n = 0;
@@ -469,6 +546,8 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &err) 
   code.resize(code_size);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
+  g_compiles++;
+  if (code_size > 0 && !path.empty()) cache_write(dir, path, code);
   return code_size > 0;
 }
 
@@ -479,7 +558,8 @@ bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *co
   std::vector<char> code;
   const Tuning tu = tuning();
   NetSpec sp = spec;  // RS_AMD_NET_CHECK_PIECES: check the 2 / 4-stripe small-shard variant
-  sp.pieces = static_cast<uint32_t>(std::max(1, std::min(4, env_int("RS_AMD_NET_CHECK_PIECES", 1))));
+  const int cp = env_int("RS_AMD_NET_CHECK_PIECES", 1);  // 1, 2 or 4 (the layouts net_pieces() produces)
+  sp.pieces = static_cast<uint32_t>(cp == 2 || cp == 4 ? cp : 1);
   const std::string name = kernel_name(sp, spec_key(sp, -1, tu)), src = generate_with(sp, name, tu);
   if (const char *dir = std::getenv("RS_AMD_JIT_DUMP")) {  // debug aid: keep the generated source
     if (FILE *f = std::fopen((std::string(dir) + "/" + name + ".hip").c_str(), "w")) {
@@ -535,6 +615,14 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const
   k->pieces = spec.pieces;
   return k;
 }
+
+// Loaded modules are never unloaded (a launch may still use one); past
+// RS_AMD_JIT_CACHE_MAX of them (default 1024) new maps run on their table kernels.
+size_t module_cap() {
+  const char *e = std::getenv("RS_AMD_JIT_CACHE_MAX");
+  return e && *e ? static_cast<size_t>(std::max(0, std::atoi(e))) : 1024u;
+}
+const char *kCapErr = "module cache full (RS_AMD_JIT_CACHE_MAX)";
 
 const Kernel *insert(const std::string &key, std::unique_ptr<Kernel> k) {  // g_mu held
   auto it = g_cache.find(key);
@@ -633,6 +721,10 @@ const Kernel *get(const NetSpec &spec, std::string &err) {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
     if (it != g_cache.end()) return it->second.get();
+    if (g_cache.size() >= module_cap()) {
+      err = kCapErr;
+      return nullptr;
+    }
   }
   std::unique_ptr<Kernel> k = build(spec, key, tu, err);
   if (!k) return nullptr;
@@ -656,6 +748,10 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
   auto f = g_failed.find(key);
   if (f != g_failed.end()) {
     err = f->second;
+    return nullptr;
+  }
+  if (g_cache.size() >= module_cap()) {
+    err = kCapErr;
     return nullptr;
   }
   pending = true;
@@ -699,6 +795,10 @@ const Kernel *get_source(const std::string &key, const std::string &name, const 
       err = f->second;
       return nullptr;
     }
+    if (g_cache.size() >= module_cap()) {
+      err = kCapErr;
+      return nullptr;
+    }
     if (async && !env_on("RS_AMD_JIT_SYNC")) {
       pending = true;
       if (g_pending.count(full)) return nullptr;
@@ -730,6 +830,15 @@ bool compile_source_check(const std::string &src, std::string &err, double *ms, 
   if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (code_bytes) *code_bytes = code.size();
   return ok;
+}
+
+void compile_stats(uint64_t *compiles, uint64_t *disk_hits, uint64_t *modules) {
+  if (compiles) *compiles = g_compiles.load();
+  if (disk_hits) *disk_hits = g_disk_hits.load();
+  if (modules) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    *modules = g_cache.size();
+  }
 }
 
 void wait_pending() {

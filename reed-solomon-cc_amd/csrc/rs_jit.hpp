@@ -91,6 +91,9 @@ const Kernel *get_source(const std::string &key, const std::string &name, const 
 // hipRTC compile of a source only (no device): a build check.
 bool compile_source_check(const std::string &src, std::string &err, double *ms, size_t *code_bytes);
 
+// hipRTC compiles run, code objects found in the disk cache, modules loaded (this process)
+void compile_stats(uint64_t *compiles, uint64_t *disk_hits, uint64_t *modules);
+
 // Block until no background compile is running (rs_net_wait).
 void wait_pending();
 

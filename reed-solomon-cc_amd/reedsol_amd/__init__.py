@@ -85,6 +85,9 @@ def lib():
         "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
         "rs_net_compile_check": (C.c_int, [u64, u64, vp, u32, vp]),
         "rs_net_wait": (C.c_int, []),
+        "rs_jit_stats": (C.c_int, [vp, vp, vp]),
+        "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
+        "rs_fft_selftest": (C.c_int, [u64, u64, u32, vp, C.c_int, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_mul_scalar": (C.c_int, [vp, sz, C.c_uint16, u32]),
@@ -311,6 +314,28 @@ def net_compile_check(k, m, present=None, flags=0) -> float:
     pres = None if present is None else (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
     _check(lib().rs_net_compile_check(k, m, pres, flags, C.byref(ms)))
     return ms.value
+
+
+def jit_stats() -> dict:
+    """hipRTC compiles, on-disk code-object cache hits and modules loaded by this process."""
+    c, h, mo = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    _check(lib().rs_jit_stats(C.byref(c), C.byref(h), C.byref(mo)))
+    return {"compiles": c.value, "cache_hits": h.value, "modules": mo.value}
+
+
+def fft_compile_check(k, m, flags=0) -> dict:
+    """Generate + hipRTC-compile the bit-sliced FFT encode kernel of a wide code (no device)."""
+    ms, b, ops = C.c_double(), C.c_uint64(), C.c_uint64()
+    _check(lib().rs_fft_compile_check(k, m, flags, C.byref(ms), C.byref(b), C.byref(ops)))
+    return {"compile_ms": ms.value, "code_bytes": b.value, "valu_ops_per_unit": ops.value}
+
+
+def fft_selftest(k, m, flags=0, skip=None, trials=8) -> int:
+    """Host check of the FFT kernel's arithmetic vs the scalar encode: mismatching symbols."""
+    bad = C.c_uint64()
+    sk = None if skip is None else (C.c_uint8 * k)(*[1 if x else 0 for x in skip])
+    _check(lib().rs_fft_selftest(k, m, flags, sk, trials, C.byref(bad)))
+    return bad.value
 
 
 def net_wait() -> None:

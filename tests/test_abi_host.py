@@ -120,21 +120,26 @@ def test_kernel_selection_network():
     present = [1] * 20
     present[3] = 0
     assert R.reconstruct_kernel_name(16, 4, 8192, present) == "net_reconstruct_i16_o1"
-    assert R.encode_kernel_name(10, 4, 2048) == "net_encode_i10_o4"  # 2 stripes per wave unit
-    assert R.encode_kernel_name(10, 4, 1024) == "net_encode_i10_o4"  # 4 stripes per wave unit
+    # 1 / 2 KiB shards: reconstructs on the networks, encodes on the table kernels unless forced
+    present4 = [0, 0, 0, 0] + [1] * 10
+    assert R.reconstruct_kernel_name(10, 4, 2048, present4) == "net_reconstruct_i10_o4"  # 2 stripes per wave unit
+    assert R.reconstruct_kernel_name(10, 4, 1024, present4) == "net_reconstruct_i10_o4"  # 4 stripes per wave unit
+    assert R.encode_kernel_name(10, 4, 2048).startswith("encode_reg_w4")
     assert R.encode_kernel_name(10, 4, 3072) == "encode_reg_w4_nv2"  # not a whole 4 KiB unit
-    assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"  # more than 16 outputs
-    # wide code, 55 erasures: the 55 x 55 syndrome map is a (background-compiled) network
-    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+net_syndrome_i55_o55"
-    # chunk 32: the register kernel beats a 300-block network (2.97 vs 3.35 ms)
-    assert R.encode_kernel_name(100, 20, 1 << 18) == "encode_reg_w32_nv1"
+    # wide codes (chunk 32 / 64): the bit-sliced FFT kernel (rs_fftnet.hpp)
+    assert R.encode_kernel_name(200, 55, 1 << 18) == "net_fft_encode_i200_o55"
+    assert R.encode_kernel_name(100, 20, 1 << 18) == "net_fft_encode_i100_o20"
+    # wide code, 55 erasures: syndromes on the FFT kernel, the 55 x 55 map a (background-compiled) network
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+net_fft_encode_i200_o55+net_syndrome_i55_o55"
 
 
 def test_kernel_selection_async_cap(monkeypatch):
     """RS_AMD_NET_ASYNC_BLOCKS=0 keeps large maps on the table kernels."""
     monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
-    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+encode_ws64_nv1+decode_mtile16_nv1"
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+net_fft_encode_i200_o55+decode_mtile16_nv1"
+    monkeypatch.setenv("RS_AMD_FFT", "0")
     assert R.encode_kernel_name(100, 20, 1 << 18) == "encode_reg_w32_nv1"
+    assert R.encode_kernel_name(200, 55, 1 << 18) == "encode_ws64_nv1"
 
 
 def test_kernel_selection(monkeypatch):
@@ -179,3 +184,37 @@ def test_small_shard_net_kernels_compile_for_gfx950(monkeypatch, pieces):
     monkeypatch.setenv("RS_AMD_NET_CHECK_PIECES", pieces)
     assert R.net_compile_check(10, 4) > 0
     assert R.net_compile_check(10, 4, [0, 0, 0, 0] + [1] * 10) > 0
+
+
+@pytest.mark.parametrize("k,m,flags", [(200, 55, 0), (200, 55, 3), (100, 20, 0), (64, 64, 1), (40, 50, 0),
+                                       (1000, 64, 0), (33, 17, 2)])
+def test_fft_kernel_arithmetic(k, m, flags):
+    """The bit-sliced FFT encode kernel's schedule with its (u, v)-coordinate matrices
+    (Cantor-basis subfield split) reproduces the codec's scalar encode, both quirk
+    modes, with and without erased (skipped) shards — host only."""
+    assert R.fft_selftest(k, m, flags, trials=6) == 0
+    skip = [1 if (i * 7) % 5 == 0 else 0 for i in range(k)]
+    assert R.fft_selftest(k, m, flags, skip=skip, trials=4) == 0
+
+
+def test_fft_kernel_compiles_for_gfx950():
+    info = R.fft_compile_check(200, 55)
+    assert info["code_bytes"] > 10000 and info["valu_ops_per_unit"] > 0
+
+
+def test_disk_code_object_cache(tmp_path):
+    """A second process compiling the same network finds the code object on disk."""
+    import os
+    import subprocess
+    import sys
+    import json
+    code = ("import sys, json; sys.path.insert(0, %r); import reedsol_amd as R; "
+            "R.net_compile_check(10, 4); print(json.dumps(R.jit_stats()))") % os.path.dirname(os.path.dirname(R.__file__))
+    env = dict(os.environ, RS_AMD_CACHE_DIR=str(tmp_path))
+    first = json.loads(subprocess.run([sys.executable, "-c", code], env=env, check=True, capture_output=True,
+                                      text=True).stdout.strip().splitlines()[-1])
+    second = json.loads(subprocess.run([sys.executable, "-c", code], env=env, check=True, capture_output=True,
+                                       text=True).stdout.strip().splitlines()[-1])
+    assert first["compiles"] >= 1 and first["cache_hits"] == 0
+    assert second["compiles"] == 0 and second["cache_hits"] >= 1
+    assert any(p.suffix == ".co" for p in tmp_path.iterdir())

@@ -297,9 +297,9 @@ def test_baseline_shapes_roundtrip(oracle, decode_mode, k, m, sb, n, erase):
     L = sb // 64
     cols = [(int(rng.integers(0, n)), int(c)) for c in rng.integers(0, L, 24)] + [(n - 1, L - 1), (0, 0)]
     sample_columns(oracle, k, m, data, par, cols)
-    if k * sb <= (64 << 10) * 4:  # small config: full oracle comparison
-        exp = oracle.encode_batch(k, m, data)
-        assert (par == exp).all()
+    # every stripe in full against the oracle's batched (AVX2, threaded) encode
+    exp = oracle.encode_batch(k, m, data, threads=16)
+    assert (par == exp).all()
     present = np.ones(k + m, np.uint8)
     present[erase] = 0
     got = gpu_reconstruct(k, m, present, data, par)
@@ -366,6 +366,34 @@ def test_host_batch_pipeline(oracle, pinned):
     out = torch.zeros((n, len(missing), sb), dtype=torch.uint8)
     R.reconstruct_batch_host(k, m, present, data, par, out)
     assert (out.numpy() == data.numpy()[:, missing]).all()
+
+
+@pytest.mark.parametrize("op", ["encode", "reconstruct"])
+def test_host_batch_error_drains_slices(oracle, monkeypatch, op):
+    """A host batch whose 4th slice fails (fault injection, RS_AMD_INJECT_HOST_FAIL):
+    the call returns the error only after the earlier slices' copies have landed
+    (every slot stream drained), and no later slice is written."""
+    k, m, sb, n = 10, 4, 1 << 16, 9
+    monkeypatch.setenv("RS_AMD_HOST_SLICE_MB", "1")  # 1 MiB / 640 KiB -> 1 stripe per slice
+    monkeypatch.setenv("RS_AMD_INJECT_HOST_FAIL", "3")
+    data = torch.from_numpy(splitmix_bytes(91, n * k * sb).reshape(n, k, sb)).pin_memory()
+    exp = oracle.encode_batch(k, m, data.numpy(), threads=4)
+    if op == "encode":
+        out = torch.zeros((n, m, sb), dtype=torch.uint8).pin_memory()
+        st = R.lib().rs_encode_batch_host(k, m, sb, n, data.data_ptr(), 0, out.data_ptr(), 0, 0)
+        want = exp
+    else:
+        present = np.array([0, 1, 0, 1, 1, 1, 1, 0, 1, 1] + [1, 1, 1, 1], np.uint8)
+        missing = [i for i in range(k) if not present[i]]
+        par = torch.from_numpy(exp).pin_memory()
+        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8).pin_memory()
+        st = R.lib().rs_reconstruct_batch_host(k, m, sb, n, present.ctypes.data, data.data_ptr(), 0, par.data_ptr(), 0,
+                                               out.data_ptr(), 0, 0)
+        want = data.numpy()[:, missing]
+    assert st == 15  # RS_ERR_DEVICE (include/reedsol.h)
+    got = out.numpy()
+    assert (got[:3] == want[:3]).all()  # slices 0..2 complete when the call returned
+    assert not got[3:].any()            # nothing from the failed slice on
 
 
 @pytest.mark.parametrize("k,m,sb", [(10, 4, 4096), (5, 5, 320), (4, 2, 2048), (16, 16, 1024), (20, 16, 512),
@@ -512,10 +540,14 @@ def test_maximum_shard_counts_vs_oracle(oracle, k, m, sb, n_lost):
 @pytest.mark.parametrize("sb", [1024, 2048])
 @pytest.mark.parametrize("k,m,n", [(10, 4, 5), (4, 2, 7), (16, 16, 3), (32, 8, 9), (6, 3, 1)])
 def test_small_shard_networks_vs_oracle(oracle, monkeypatch, sb, k, m, n):
-    """1 / 2 KiB shards on the network kernels (wave units span 4 / 2 stripes; stripe
-    counts that are no multiple of that leave pieces past the batch unstored):
-    encode bit-exact vs the oracle, reconstruct restores the erased originals, and
-    the result equals the table kernels' (RS_AMD_NET_SMALL=0)."""
+    """1 / 2 KiB shards on the network kernels (wave units span 4 / 2 stripes; for stripe
+    counts that are no multiple of that, pieces past the batch are clamped to the last
+    stripe of their wave unit and rewrite identical bytes, so nothing past row n is
+    touched — the guard row checks it): encode (forced on, RS_AMD_NET_SMALL_ENCODE=1;
+    encodes of small shards default to the table kernels) bit-exact vs the oracle,
+    reconstruct restores the erased originals, and both equal the table kernels'
+    (RS_AMD_NET_SMALL=0)."""
+    monkeypatch.setenv("RS_AMD_NET_SMALL_ENCODE", "1")
     assert R.encode_kernel_name(k, m, sb).startswith("net_encode"), R.encode_kernel_name(k, m, sb)
     rng = np.random.default_rng(k * 131 + m + sb)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
@@ -542,3 +574,59 @@ def test_small_shard_networks_vs_oracle(oracle, monkeypatch, sb, k, m, n):
     R.encode_batch_dev(k, m, d, p2)
     torch.cuda.synchronize()
     assert torch.equal(p2, p[:n])
+
+
+@pytest.mark.parametrize("sb", [1024, 2048])
+@pytest.mark.parametrize("n", [5, 7])
+def test_small_shard_syndrome_network(oracle, monkeypatch, sb, n):
+    """RS(200,55) losing 32 data shards at 1 / 2 KiB shards: the syndrome path's e x e
+    map on its small-shard network variant (inputs rec ^ scratch per 1 KiB piece),
+    compiled synchronously; ragged stripe counts with a guard row; == table kernels."""
+    monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")
+    k, m = 200, 55
+    rng = np.random.default_rng(sb + n)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=8)
+    lost = sorted(int(i) for i in rng.choice(k, size=32, replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    name = R.reconstruct_kernel_name(k, m, sb, present)
+    assert "net_syndrome" in name, name
+    guard = 0x5A
+    out = torch.full((n + 1, 32, sb), guard, dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, to_dev(data), to_dev(par), out[:n])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out[:n].cpu().numpy(), data[:, lost])
+    assert (out[n].cpu().numpy() == guard).all()
+    monkeypatch.setenv("RS_AMD_NET_SMALL", "0")
+    assert gpu_reconstruct(k, m, present, data, par).tobytes() == out[:n].cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("sb", [1024, 2048])
+@pytest.mark.parametrize("k,m,n", [(16, 64, 5), (10, 20, 7)])
+def test_small_shard_lowrate_networks(oracle, monkeypatch, sb, k, m, n):
+    """Low-rate maps (up to 64 outputs, several 8-output tiles) on the small-shard network
+    variants, JIT on and compiled synchronously: encode == oracle restatement (parity
+    unpinned: the reference has no low-rate codec), reconstruct restores the data,
+    both equal the table kernels (RS_AMD_NET_SMALL=0)."""
+    monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")
+    monkeypatch.setenv("RS_AMD_NET_SMALL_ENCODE", "1")
+    rng = np.random.default_rng(k * 7 + m + sb)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = oracle.encode_low_batch(k, m, data) if hasattr(oracle, "encode_low_batch") else None
+    p = gpu_encode(k, m, data)
+    if exp is not None:
+        np.testing.assert_array_equal(p, exp)
+    else:
+        for s in range(n):
+            st, e = oracle.encode_low(k, m, data[s])
+            assert st == 0
+            np.testing.assert_array_equal(p[s], e)
+    lost = sorted(int(i) for i in rng.choice(k, size=min(k, m) // 2 + 1, replace=False))
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    got = gpu_reconstruct(k, m, present, data, p)
+    np.testing.assert_array_equal(got, data[:, lost])
+    monkeypatch.setenv("RS_AMD_NET_SMALL", "0")
+    assert (gpu_encode(k, m, data) == p).all()
+    assert (gpu_reconstruct(k, m, present, data, p) == got).all()

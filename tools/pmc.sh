@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-ARGS=${PMC_ARGS:---steps 2 --warmup 1 --cpu-seconds 0 --stripes 1024 --no-verify}
+ARGS=${PMC_ARGS:---steps 2 --warmup 1 --cpu-seconds 0 --stripes 4096 --no-verify}
 for c in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $c"
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc/$c" -o run -- \

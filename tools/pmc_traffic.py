@@ -17,9 +17,12 @@ import statistics
 
 
 def short_name(full):
-    m = re.search(r"rs_net_(encode|reconstruct)_i(\d+)_o(\d+)_[0-9a-f]+", full)
+    m = re.search(r"rs_net_(encode|reconstruct|syndrome)_i(\d+)_o(\d+)_[0-9a-f]+", full)
     if m:
         return f"net_{m.group(1)}_i{m.group(2)}_o{m.group(3)}"
+    m = re.search(r"rs_fft_encode_k(\d+)_m(\d+)_[0-9a-f]+", full)
+    if m:
+        return f"net_fft_encode_i{m.group(1)}_o{m.group(2)}"
     m = re.search(r"k_(encode_reg|decode_reg|decode_matrix)<(\d+), (\d+)>", full)
     if m:
         kind, size, nv = m.groups()
@@ -53,15 +56,23 @@ def main():
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--e", type=int, default=4)
     ap.add_argument("--shard-bytes", type=int, default=1 << 20)
+    ap.add_argument("--only", default="", help="comma list of kernel short names to record (default all)")
+    ap.add_argument("--alg-shards", type=int, default=0, help="algorithmic shard passes per stripe (override)")
     a = ap.parse_args()
     fetch, write = read(a.pmc_dir, "FETCH_SIZE"), read(a.pmc_dir, "WRITE_SIZE")
     out = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    only = {x for x in a.only.split(",") if x}
     for n in sorted(set(fetch) & set(write)):
+        if only and n not in only:
+            continue
         f, w = 2.0 * fetch[n], write[n]
-        alg = ((a.k + a.m) if n.startswith(("encode", "net_encode")) else (a.k + a.e)) * a.shard_bytes
+        alg = ((a.k + a.m) if n.startswith(("encode", "net_encode", "net_fft_encode")) else (a.k + a.e)) * a.shard_bytes
+        if a.alg_shards:
+            alg = a.alg_shards * a.shard_bytes
         out[n] = {"fetch_bytes_per_stripe": f / a.stripes, "write_bytes_per_stripe": w / a.stripes,
                   "hbm_bytes_per_stripe": (f + w) / a.stripes, "algorithmic_bytes_per_stripe": alg,
                   "traffic_over_algorithmic": round((f + w) / a.stripes / alg, 4),
+                  "hbm_bytes_per_launch": f + w, "stripes_per_launch": a.stripes,
                   "workload": f"RS({a.k},{a.m}) {a.shard_bytes} B shards, {a.stripes} stripes per launch",
                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH_SIZE x2 (gfx950)"}
         print(n, json.dumps(out[n]))
