@@ -159,6 +159,22 @@ int rs_reconstruct_batch_host(uint64_t original_count, uint64_t recovery_count, 
                               uint64_t recovery_stripe_stride, void *h_restored, uint64_t restored_stripe_stride,
                               uint32_t flags);
 
+/* The same host-memory batches split over several GPUs of the node: device i of
+ * devices[0..n_devices) (NULL = every visible device) takes the contiguous stripe
+ * range [i*n/D, (i+1)*n/D) and runs it on its own worker thread and staging ring
+ * (stripes are independent: no exchange between devices). Returns the first
+ * failing device's status (its message in rs_last_error) after every worker ended. */
+int rs_encode_batch_host_multi(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                               uint64_t n_stripes, const void *h_original, uint64_t original_stripe_stride,
+                               void *h_recovery, uint64_t recovery_stripe_stride, uint32_t flags,
+                               const int *devices, int n_devices);
+int rs_reconstruct_batch_host_multi(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                                    uint64_t n_stripes, const uint8_t *present, const void *h_original,
+                                    uint64_t original_stripe_stride, const void *h_recovery,
+                                    uint64_t recovery_stripe_stride, void *h_restored,
+                                    uint64_t restored_stripe_stride, uint32_t flags, const int *devices,
+                                    int n_devices);
+
 /* Which device kernel a call would run on ("net_encode_i10_o4", "encode_reg_w4_nv4",
  * "decode_matrix_e4_nv4", "encode_generic_nv1", ...), assuming 16-byte aligned buffers.
  * present: k+m flags as for rs_reconstruct_batch_dev, or NULL for "the first min(k, m)

@@ -17,6 +17,7 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/reedsol.h"
@@ -1798,6 +1799,79 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
       return RS_OK;
     };
     return drain_after(p, slices());
+  });
+}
+
+}  // extern "C"
+
+namespace {
+// One worker thread per device over contiguous stripe ranges (sharding.stripe_range's
+// partition); each worker selects its device and calls the single-device host batch.
+template <class F>
+int run_multi(uint64_t n, const int *devices, int n_devices, F &&one) {
+  std::vector<int> devs;
+  if (devices) {
+    if (n_devices <= 0) return fail(RS_ERR_INVALID_ARGUMENT, "n_devices <= 0");
+    devs.assign(devices, devices + n_devices);
+  } else {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) return fail(RS_ERR_NO_DEVICE, "no HIP device");
+    for (int d = 0; d < cnt; d++) devs.push_back(d);
+  }
+  const uint64_t D = devs.size();
+  std::vector<int> status(D, RS_OK);
+  std::vector<std::string> msg(D);
+  std::vector<std::thread> th;
+  th.reserve(D);
+  for (uint64_t i = 0; i < D; i++) {
+    const uint64_t b = n * i / D, e = n * (i + 1) / D;
+    th.emplace_back([&, i, b, e] {
+      if (hipSetDevice(devs[i]) != hipSuccess) {
+        status[i] = RS_ERR_NO_DEVICE;
+        msg[i] = "hipSetDevice(" + std::to_string(devs[i]) + ") failed";
+        return;
+      }
+      status[i] = e > b ? one(b, e - b) : RS_OK;
+      if (status[i]) msg[i] = rs_last_error();
+    });
+  }
+  for (auto &t : th) t.join();
+  for (uint64_t i = 0; i < D; i++)
+    if (status[i]) return fail(status[i], "device " + std::to_string(devs[i]) + ": " + msg[i]);
+  return RS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rs_encode_batch_host_multi(uint64_t k, uint64_t m, size_t sb, uint64_t n, const void *h_orig, uint64_t orig_stride,
+                               void *h_rec, uint64_t rec_stride, uint32_t flags, const int *devices, int n_devices) {
+  return guarded([&]() -> int {
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    return run_multi(n, devices, n_devices, [&](uint64_t s0, uint64_t cnt) {
+      return rs_encode_batch_host(k, m, sb, cnt, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride,
+                                  orig_stride, static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, flags);
+    });
+  });
+}
+
+int rs_reconstruct_batch_host_multi(uint64_t k, uint64_t m, size_t sb, uint64_t n, const uint8_t *present,
+                                    const void *h_orig, uint64_t orig_stride, const void *h_rec, uint64_t rec_stride,
+                                    void *h_out, uint64_t out_stride, uint32_t flags, const int *devices,
+                                    int n_devices) {
+  return guarded([&]() -> int {
+    if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+    uint64_t e = 0;
+    for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+    if (orig_stride == 0) orig_stride = k * sb;
+    if (rec_stride == 0) rec_stride = m * sb;
+    if (out_stride == 0) out_stride = e * sb;
+    return run_multi(n, devices, n_devices, [&](uint64_t s0, uint64_t cnt) {
+      return rs_reconstruct_batch_host(k, m, sb, cnt, present, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride,
+                                       orig_stride, static_cast<const uint8_t *>(h_rec) + s0 * rec_stride, rec_stride,
+                                       static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, flags);
+    });
   });
 }
 

@@ -81,6 +81,9 @@ def lib():
                                                         vp, u32, vp]),
         "rs_encode_batch_host": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32]),
         "rs_reconstruct_batch_host": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32]),
+        "rs_encode_batch_host_multi": (C.c_int, [u64, u64, sz, u64, vp, u64, vp, u64, u32, vp, C.c_int]),
+        "rs_reconstruct_batch_host_multi": (C.c_int, [u64, u64, sz, u64, vp, vp, u64, vp, u64, vp, u64, u32, vp,
+                                                      C.c_int]),
         "rs_encode_kernel_name": (C.c_char_p, [u64, u64, sz]),
         "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
         "rs_net_compile_check": (C.c_int, [u64, u64, vp, u32, vp]),
@@ -273,6 +276,32 @@ def reconstruct_batch_host(original_count: int, recovery_count: int, present, or
     _check(lib().rs_reconstruct_batch_host(original_count, recovery_count, sb, n, pres,
                                            C.c_void_p(_host_ptr(original)), 0, C.c_void_p(_host_ptr(recovery)), 0,
                                            C.c_void_p(_host_ptr(restored)), 0, flags))
+
+
+def _devices(devices):
+    if devices is None:
+        return None, 0
+    arr = (C.c_int * len(devices))(*devices)
+    return arr, len(devices)
+
+
+def encode_batch_host_multi(original_count: int, recovery_count: int, data, parity, devices=None,
+                            flags: int = FLAG_CORRECTED):
+    """Host batch split over several GPUs (contiguous stripe ranges, one worker per device)."""
+    n, k, sb = data.shape
+    dv, nd = _devices(devices)
+    _check(lib().rs_encode_batch_host_multi(original_count, recovery_count, sb, n, C.c_void_p(_host_ptr(data)), 0,
+                                            C.c_void_p(_host_ptr(parity)), 0, flags, dv, nd))
+
+
+def reconstruct_batch_host_multi(original_count: int, recovery_count: int, present, original, recovery, restored,
+                                 devices=None, flags: int = FLAG_CORRECTED):
+    n, k, sb = original.shape
+    pres = (C.c_uint8 * (original_count + recovery_count))(*[1 if p else 0 for p in present])
+    dv, nd = _devices(devices)
+    _check(lib().rs_reconstruct_batch_host_multi(original_count, recovery_count, sb, n, pres,
+                                                 C.c_void_p(_host_ptr(original)), 0, C.c_void_p(_host_ptr(recovery)),
+                                                 0, C.c_void_p(_host_ptr(restored)), 0, flags, dv, nd))
 
 
 def _host_ptr(a) -> int:

@@ -368,6 +368,24 @@ def test_host_batch_pipeline(oracle, pinned):
     assert (out.numpy() == data.numpy()[:, missing]).all()
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0], [0, 0, 0]])
+def test_host_batch_multi_device(oracle, devices):
+    """rs_*_batch_host_multi: contiguous stripe ranges, one worker thread + staging
+    ring per listed device (here the box's one GPU listed several times, so the
+    workers share its ring and run concurrently through the C ABI) == oracle."""
+    k, m, sb, n = 10, 4, 1 << 16, 11
+    data = torch.from_numpy(splitmix_bytes(5, n * k * sb).reshape(n, k, sb)).pin_memory()
+    par = torch.zeros((n, m, sb), dtype=torch.uint8).pin_memory()
+    R.encode_batch_host_multi(k, m, data, par, devices)
+    exp = oracle.encode_batch(k, m, data.numpy(), threads=4)
+    assert (par.numpy() == exp).all()
+    present = [1, 0, 1, 1, 0, 1, 1, 1, 1, 0] + [1, 1, 1, 1]
+    missing = [i for i in range(k) if not present[i]]
+    out = torch.zeros((n, len(missing), sb), dtype=torch.uint8).pin_memory()
+    R.reconstruct_batch_host_multi(k, m, present, data, par, out, devices)
+    assert (out.numpy() == data.numpy()[:, missing]).all()
+
+
 @pytest.mark.parametrize("op", ["encode", "reconstruct"])
 def test_host_batch_error_drains_slices(oracle, monkeypatch, op):
     """A host batch whose 4th slice fails (fault injection, RS_AMD_INJECT_HOST_FAIL):
