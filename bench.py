@@ -89,6 +89,7 @@ def cpu_baseline(k, m, sb, erase, budget_s):
     # c4: RS(200,55) 256 KiB, 55 erased data shards (every third), threads stripes
     c4_erase = list(range(1, 200, 3))[:55]
     v4, e4, r4 = _cpu_leg(O, 200, 55, 256 << 10, c4_erase, threads, threads, rng)
+    _, e41, r41 = _cpu_leg(O, 200, 55, 256 << 10, c4_erase, 1, 1, rng)
     return {
         "value": round(vt, 3),
         "unit": "GiB/s",
@@ -108,6 +109,8 @@ def cpu_baseline(k, m, sb, erase, budget_s):
             "c4 RS(200,55) 256KiB encode GiB/s": round(e4, 3),
             "c4 RS(200,55) 256KiB reconstruct55 GiB/s": round(r4, 3),
             "c4 sample": f"{threads} stripes, {threads} threads",
+            "c4 RS(200,55) 256KiB encode GiB/s 1 thread": round(e41, 3),
+            "c4 RS(200,55) 256KiB reconstruct55 GiB/s 1 thread": round(r41, 3),
         },
         "harness": harness_protocol(O),
         "cpu_model": _cpu_model(),
