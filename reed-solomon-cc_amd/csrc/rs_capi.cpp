@@ -81,16 +81,18 @@ int use_high_rate(uint64_t original, uint64_t recovery) {
   return original <= recovery ? 1 : 0;
 }
 
-constexpr uint64_t kLowRateMaxRecovery = 64;
-inline bool recovery_ok_low_rate(uint64_t m) { return m <= kLowRateMaxRecovery; }
+// Low rate runs as maps of k x m GF(2^16) constants (passes of <= 64 outputs): the
+// map size bounds the tables (96 B per entry) and the reconstruct's 16e x 16e solve.
+constexpr uint64_t kLowRateMaxMap = 1ull << 16;
+inline bool low_rate_ok(uint64_t k, uint64_t m) { return k * m <= kLowRateMaxMap; }
 
 // Encoder.init / Decoder.init checks (root.zig:100-103, 198-201) + the tail panic (root.zig:385)
 int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
   const int hr = use_high_rate(k, m);
   if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
-  // low rate: the reference panics (root.zig:120); here up to 64 recovery shards (§8 f4)
-  if (hr == 0 && recovery_ok_low_rate(m) == false)
-    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec with more than 64 recovery shards");
+  // low rate: the reference panics (root.zig:120); here maps with k * m <= 65536 (§8 f4)
+  if (hr == 0 && !low_rate_ok(k, m))
+    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec with original_count * recovery_count > 65536");
   if (shard_bytes == 0 || (shard_bytes & 1)) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes is 0 or odd");
   // shard_bytes % 64 != 0: the reference panics (root.zig:385); handled here with
   // the tail layout of root.zig:338-348 (tail_* below).
@@ -156,9 +158,10 @@ void warn_once_per_reason(const char *what, const std::string &err) {
 // Bit-sliced FFT kernel of a plan (rs_fftnet.hpp): wide codes, compiled on first use.
 struct FftSlot {
   std::mutex mu;
-  bool failed = false;
+  bool failed[2] = {false, false};  // per variant: 2 KiB units of one stripe / of two 1 KiB stripes
   bool async = false;  // per-pattern kernels: background compile, the table encode meanwhile
   fftnet::Spec spec;
+  fftnet::Spec spec_p2;  // the 1 KiB-shard variant (Spec::pieces 2), filled on first use
 };
 
 bool fft_enabled() {
@@ -166,16 +169,24 @@ bool fft_enabled() {
   return jit::enabled() && !(e && std::strcmp(e, "0") == 0);
 }
 
-const jit::Kernel *fft_kernel(FftSlot &slot) {
+// The slot's kernel for shards of sb bytes; *used = the spec to launch it with.
+const jit::Kernel *fft_kernel(FftSlot &slot, uint64_t sb, const fftnet::Spec **used) {
   std::lock_guard<std::mutex> lk(slot.mu);
-  if (slot.failed) return nullptr;
+  const int vi = fftnet::pieces(sb) > 1 ? 1 : 0;
+  if (slot.failed[vi]) return nullptr;
+  if (vi && slot.spec_p2.pieces == 1) {
+    slot.spec_p2 = slot.spec;
+    slot.spec_p2.pieces = 2;
+  }
+  const fftnet::Spec &spec = vi ? slot.spec_p2 : slot.spec;
+  *used = &spec;
   std::string err;
   bool pending = false;
   const char *a = std::getenv("RS_AMD_FFT_ASYNC");
   const bool async = a && *a ? std::strcmp(a, "0") != 0 : slot.async;
-  const jit::Kernel *k = fftnet::get(slot.spec, async, err, pending);
+  const jit::Kernel *k = fftnet::get(spec, async, err, pending);
   if (!k && !pending) {
-    slot.failed = true;
+    slot.failed[vi] = true;
     warn_once_per_reason("[rs_amd] bit-sliced FFT kernel unavailable, using table kernels: ", err);
   }
   return k;
@@ -766,15 +777,23 @@ int linear_decode_map(uint64_t k, uint64_t m, const jit::NetSpec &G, const uint8
   return RS_OK;
 }
 
-// A map on the device: the network kernel when it fits, else the table matrix
+// A map on the device, in passes of <= 64 outputs (jit::kMaxOut; every pass reads
+// all inputs): per pass the network kernel when it fits, else the table matrix
 // kernels over groups of <= 8 outputs (blocks [group][n_in][E_g] of tables + src).
 struct MapPlan {
   std::shared_ptr<DevBuf> buf;
   uint32_t n_in = 0, n_out = 0;
   std::vector<size_t> group_off;  // byte offset of each group's table block
   size_t off_src = 0;
-  std::shared_ptr<NetSlot> net;
+  std::vector<std::shared_ptr<NetSlot>> net;  // per pass: outputs [64 p, 64 p + 64)
 };
+
+inline uint32_t map_passes(uint32_t n_out) { return (n_out + jit::kMaxOut - 1) / jit::kMaxOut; }
+// every pass of an n_in x n_out map has a network form (the first pass is the widest)
+bool map_net_ok(uint64_t n_in, uint64_t n_out, uint64_t sb) {
+  return jit::enabled() && n_out > 0 &&
+         jit::supports_async(static_cast<uint32_t>(n_in), static_cast<uint32_t>(std::min<uint64_t>(n_out, jit::kMaxOut)), sb);
+}
 PlanCache<MapPlan> g_map_plans;
 
 int build_map_plan(int dev, jit::NetSpec &&spec, std::shared_ptr<MapPlan> &out) {
@@ -795,25 +814,53 @@ int build_map_plan(int dev, jit::NetSpec &&spec, std::shared_ptr<MapPlan> &out) 
   p->off_src = tabs.size() * sizeof(RsTab);
   int st = upload(blob.data(), blob.size(), dev, p->buf);
   if (st) return st;
-  p->net = std::make_shared<NetSlot>();
-  p->net->async = !jit::supports(p->n_in, p->n_out, jit::kUnitBytes);  // larger maps: background compile
-  p->net->spec = std::move(spec);
+  for (uint32_t j0 = 0; j0 < spec.n_out; j0 += jit::kMaxOut) {
+    const uint32_t len = std::min<uint32_t>(jit::kMaxOut, spec.n_out - j0);
+    auto slot = std::make_shared<NetSlot>();
+    slot->async = !jit::supports(p->n_in, len, jit::kUnitBytes);  // larger maps: background compile
+    jit::NetSpec &ps = slot->spec;
+    ps.role = spec.role;
+    ps.n_in = spec.n_in;
+    ps.n_out = len;
+    ps.src = spec.src;
+    if (len == spec.n_out) {
+      ps.images = std::move(spec.images);
+    } else {
+      ps.images.resize(static_cast<size_t>(spec.n_in) * len * 16);
+      for (uint32_t t = 0; t < spec.n_in; t++)
+        std::memcpy(&ps.images[static_cast<size_t>(t) * len * 16],
+                    &spec.images[(static_cast<size_t>(t) * spec.n_out + j0) * 16], len * 16 * sizeof(uint16_t));
+    }
+    p->net.push_back(std::move(slot));
+  }
   out = p;
   return RS_OK;
 }
+
+int run_map_pass(const MapPlan &p, uint32_t pi, bool net_ok, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0,
+                 const uint8_t *b1, uint64_t s1, uint8_t *out, uint64_t so, int max_nv, hipStream_t s);
 
 // out[j] = sum_i map_ij(in_i) for every stripe; inputs per src (buffer 0 / 1).
 int run_map(const MapPlan &p, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0, const uint8_t *b1, uint64_t s1,
             uint8_t *out, uint64_t so, int max_nv, hipStream_t s) {
   if (!b0) b0 = b1;
   if (!b1) b1 = b0;
-  if (max_nv == 4 && jit::enabled() && jit::supports_async(p.n_in, p.n_out, sb))
-    if (const jit::Kernel *nk = net_kernel(*p.net, sb)) {
-      HIP_TRY(jit::launch(*nk, b0, s0, b1, s1, out, so, sb, n, s));
+  const bool net_ok = max_nv == 4 && map_net_ok(p.n_in, p.n_out, sb);
+  for (uint32_t pi = 0; pi < p.net.size(); pi++)
+    if (int st = run_map_pass(p, pi, net_ok, sb, n, b0, s0, b1, s1, out, so, max_nv, s)) return st;
+  return RS_OK;
+}
+
+int run_map_pass(const MapPlan &p, uint32_t pi, bool net_ok, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0,
+                 const uint8_t *b1, uint64_t s1, uint8_t *out, uint64_t so, int max_nv, hipStream_t s) {
+  const uint32_t p0 = pi * jit::kMaxOut, p1 = std::min<uint32_t>(p.n_out, p0 + jit::kMaxOut);
+  if (net_ok)
+    if (const jit::Kernel *nk = net_kernel(*p.net[pi], sb)) {
+      HIP_TRY(jit::launch(*nk, b0, s0, b1, s1, out + static_cast<uint64_t>(p0) * sb, so, sb, n, s));
       return RS_OK;
     }
   const uint8_t *base = static_cast<const uint8_t *>(p.buf->p);
-  for (size_t g = 0; g < p.group_off.size(); g++) {
+  for (size_t g = p0 / kMatrixMaxOut; g < p.group_off.size() && g * kMatrixMaxOut < p1; g++) {
     const uint32_t j0 = static_cast<uint32_t>(g * kMatrixMaxOut);
     const uint32_t eg = std::min<uint32_t>(kMatrixMaxOut, p.n_out - j0);
     const KernelChoice kc = choose_decode_matrix(eg, sb, max_nv);
@@ -1018,8 +1065,7 @@ static const char *net_name(const char *role, uint64_t n_in, uint64_t n_out) {
 
 const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
   if (is_low_rate(k, m)) {
-    if (jit::enabled() && jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))
-      return net_name("encode_low", k, m);
+    if (map_net_ok(k, m, sb)) return net_name("encode_low", k, m);
     return "lowrate_matrix";
   }
   if (fft_enabled() && fftnet::supports(k, m, sb)) return net_name("fft_encode", k, m);
@@ -1038,8 +1084,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
   if (is_low_rate(k, m)) {
-    if (jit::enabled() && jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
-      return net_name("reconstruct_low", k, e);
+    if (map_net_ok(k, e, sb)) return net_name("reconstruct_low", k, e);
     return "lowrate_matrix";
   }
   const std::string mode = decode_mode_env();
@@ -1091,6 +1136,8 @@ int rs_fft_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compile
     spec.k = static_cast<uint32_t>(k);
     spec.m = static_cast<uint32_t>(m);
     spec.flags = flags;
+    // RS_AMD_FFT_CHECK_PIECES=2: the 1 KiB-shard variant (units of two stripes)
+    if (const char *pc = std::getenv("RS_AMD_FFT_CHECK_PIECES")) spec.pieces = std::strcmp(pc, "2") == 0 ? 2 : 1;
     if (valu_ops) {
       const fftnet::Stats s = fftnet::stats(spec);
       *valu_ops = s.ops_a + s.ops_b + s.ops_io;
@@ -1184,8 +1231,9 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
     std::shared_ptr<EncodePlan> plan;
     if ((st = get_encode_plan(dev, k, m, flags, plan))) return st;
     if (max_nv == 4 && plan->fft && fft_enabled() && fftnet::supports(k, m, sb)) {
-      if (const jit::Kernel *fk = fft_kernel(*plan->fft)) {
-        HIP_TRY(fftnet::launch(*fk, plan->fft->spec, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
+      const fftnet::Spec *fs = nullptr;
+      if (const jit::Kernel *fk = fft_kernel(*plan->fft, sb, &fs)) {
+        HIP_TRY(fftnet::launch(*fk, *fs, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
                                static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));
         return RS_OK;
       }
@@ -1359,9 +1407,10 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
         db.xsrc_stripe_stride = m * sb;
         db.n_stripes = cnt;
         hipError_t err = hipSuccess;
-        const jit::Kernel *fk = plan->syn_fft && max_nv == 4 ? fft_kernel(*plan->syn_fft) : nullptr;
+        const fftnet::Spec *fs = nullptr;
+        const jit::Kernel *fk = plan->syn_fft && max_nv == 4 ? fft_kernel(*plan->syn_fft, sb, &fs) : nullptr;
         if (fk)
-          err = fftnet::launch(*fk, plan->syn_fft->spec, eb.data, orig_stride, nullptr, 0, eb.parity, m * sb, sb, cnt, s);
+          err = fftnet::launch(*fk, *fs, eb.data, orig_stride, nullptr, 0, eb.parity, m * sb, sb, cnt, s);
         else
           err = launch_encode(ke, eb, s);
         if (err == hipSuccess) {

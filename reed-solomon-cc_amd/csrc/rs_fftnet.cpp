@@ -510,9 +510,30 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // default both: RS(200,55) 256 KiB encode 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
   const int nt = nt_of();
   o << "#define RS_AUX_LD " << ((nt & 1) ? 2 : 0) << "\n#define RS_AUX_ST " << ((nt & 2) ? 2 : 0) << "\n" << kPrelude;
+  // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
+  // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
+  // batch, so its loads read zeros and its stores are dropped)
+  const bool two = s.pieces == 2;
+  auto rsrc = [&](const char *base, const char *stride, const std::string &stripe, uint32_t rows) {
+    return std::string("__builtin_amdgcn_make_buffer_rsrc((void *)(") + base + " + (" + stripe + ") * " + stride +
+           "), (short)0, (int)(" + std::to_string(rows) + "u * sbl), 0x00020000)";
+  };
+  // name = rsrc(stripe0) [, name1 = rsrc(stripe0 + 1) or RZ]; `guard`: the unit exists
+  auto rsrc_pair = [&](std::ostream &os_, const char *name, const char *base, const char *stride, const std::string &st0,
+                       uint32_t rows, const std::string &guard) {
+    const std::string s0 = two ? "(" + st0 + ") * 2u" : st0;
+    os_ << "  const __amdgpu_buffer_rsrc_t " << name << " = " << (guard.empty() ? "" : guard + " ? ")
+        << rsrc(base, stride, s0, rows) << (guard.empty() ? "" : " : RZ") << ";\n";
+    if (two)
+      os_ << "  const __amdgpu_buffer_rsrc_t " << name << "1 = " << (guard.empty() ? "" : guard + " && ") << s0
+          << " + 1u < n_st ? " << rsrc(base, stride, s0 + " + 1u", rows) << " : RZ;\n";
+    else
+      os_ << "  const __amdgpu_buffer_rsrc_t " << name << "1 = " << name << ";\n";
+  };
+  const char *half = two ? "loff" : "uo + 1024u";  // offset of a unit's second KiB
   o << "extern \"C\" __global__ __launch_bounds__(" << NW * 64 << ") void " << name
     << "(const unsigned char *__restrict__ data, u64 ds, const unsigned char *__restrict__ rec, u64 rs,\n"
-       "    unsigned char *__restrict__ out, u64 os, u32 sb, u32 ups, u64 n_units) {\n"
+       "    unsigned char *__restrict__ out, u64 os, u32 sb, u32 ups, u64 n_units, u64 n_st) {\n"
     << "  __shared__ u32 xch[" << C * 8 * 64 << "];\n"
     << "  v4 *const xch4 = (v4 *)xch;\n"
     << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
@@ -525,25 +546,18 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
        "  const __amdgpu_buffer_rsrc_t RZ = __builtin_amdgcn_make_buffer_rsrc((void *)data, (short)0, 0, 0x00020000);\n"
        "  v4 la0[8], lb0[8];\n"
        "  {  // prologue: the first unit's leading positions of chunk 0\n"
-       "  const u32 sbl = sb, uo = uu * 2048u + loff, uo1 = uo + 1024u;\n"
-    << "  const __amdgpu_buffer_rsrc_t RD = blockIdx.x < n_units ? __builtin_amdgcn_make_buffer_rsrc((void *)(data + "
-       "stripe * ds), (short)0, (int)("
-    << s.k << "u * sbl), 0x00020000) : RZ;\n";
+       "  const u32 sbl = sb, uo = uu * 2048u + loff, uo1 = " << half << ";\n";
+  rsrc_pair(o, "RD", "data", "ds", "stripe", s.k, "blockIdx.x < n_units");
   // (loads emitted below, once emit_loads exists)
   std::ostringstream hdr2;
   hdr2 << "#pragma unroll 1\n"
        "  for (u64 u = blockIdx.x; u < n_units; u += gridDim.x) {\n"
        "  u32 sbl = sb;\n"
        "  asm volatile(\"\" : \"+s\"(sbl));  // shard offsets are recomputed per unit (SALU), not hoisted into VGPRs\n"
-       "  const u32 uo = uu * 2048u + loff, uo1 = uo + 1024u;\n"
-    << "  const __amdgpu_buffer_rsrc_t RD = __builtin_amdgcn_make_buffer_rsrc((void *)(data + stripe * ds), (short)0, (int)("
-    << s.k << "u * sbl), 0x00020000);\n"
-    << "  const __amdgpu_buffer_rsrc_t RO = __builtin_amdgcn_make_buffer_rsrc((void *)(out + stripe * os), (short)0, (int)("
-    << s.m << "u * sbl), 0x00020000);\n";
-  if (any_xor)
-    hdr2 << "  const __amdgpu_buffer_rsrc_t RR = __builtin_amdgcn_make_buffer_rsrc((void *)(rec + stripe * rs), (short)0, "
-         "(int)("
-      << s.m << "u * sbl), 0x00020000);\n";
+       "  const u32 uo = uu * 2048u + loff, uo1 = " << half << ";\n";
+  rsrc_pair(hdr2, "RD", "data", "ds", "stripe", s.k, "");
+  rsrc_pair(hdr2, "RO", "out", "os", "stripe", s.m, "");
+  if (any_xor) rsrc_pair(hdr2, "RR", "rec", "rs", "stripe", s.m, "");
   hdr2 << "  u32 ";
   for (uint32_t r = 0; r < 8; r++)
     for (int i = 0; i < 8; i++) hdr2 << "w" << r << "_" << i << ", b" << r << "_" << i << ", c" << r << "_" << i << (r == 7 && i == 7 ? ";\n" : ", ");
@@ -592,8 +606,10 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     if (!full) o << "  const u32 vm = " << mask_expr(vm) << ";\n";
     for (uint32_t r = r0; r < r1; r++) {
       o << "  { const u32 so = (" << j * C + r << "u + (w << 3)) * sbl;\n    ";
+      const std::string rd1 = std::string(rd) + "1";
       const std::string rs = full ? std::string(rd) : "((vm >> " + std::to_string(r) + " & 1u) ? " + rd + " : RZ)";
-      o << "la" << j << "[" << r << "] = LDB(" << rs << ", " << uo0 << ", so); lb" << j << "[" << r << "] = LDB(" << rs
+      const std::string rs1 = full ? rd1 : "((vm >> " + std::to_string(r) + " & 1u) ? " + rd1 + " : RZ)";
+      o << "la" << j << "[" << r << "] = LDB(" << rs << ", " << uo0 << ", so); lb" << j << "[" << r << "] = LDB(" << rs1
         << ", " << uo1 << ", so); }\n";
     }
     o << "  }\n  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_sched_barrier(0);\n";
@@ -731,10 +747,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // the next unit's leading chunk-0 positions, in flight during this unit's last exchange and stores
   o << "  u64 stripe_n = stripe + gdiv;\n  u32 uu_n = uu + gmod;\n  if (uu_n >= ups) { uu_n -= ups; stripe_n++; }\n";
   if (pf && xunit) {
-    o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = uon + 1024u;\n"
-      << "  const __amdgpu_buffer_rsrc_t RDn = u + gridDim.x < n_units ? __builtin_amdgcn_make_buffer_rsrc((void *)(data + "
-         "stripe_n * ds), (short)0, (int)("
-      << s.k << "u * sbl), 0x00020000) : RZ;\n";
+    o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = " << (two ? "loff" : "uon + 1024u") << ";\n";
+    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, "u + gridDim.x < n_units");
     emit_loads(0, 0, pf, "RDn", "uon", "uon1");
     o << "  }\n";
   }
@@ -794,8 +808,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       o << "    v4 a, b; unplanes2(Q, a, b);\n";
       g.op(4 + 48);
       o << "    const u32 so = " << p << "u * sbl;\n";
-      if (P.out_mode[p] == kOutXorRec) o << "    a ^= LDB(RR, uo, so); b ^= LDB(RR, uo1, so);\n";
-      o << "    STB(a, RO, uo, so); STB(b, RO, uo1, so); }\n";
+      if (P.out_mode[p] == kOutXorRec) o << "    a ^= LDB(RR, uo, so); b ^= LDB(RR1, uo1, so);\n";
+      o << "    STB(a, RO, uo, so); STB(b, RO1, uo1, so); }\n";
     }
     g.ops = &g.st->ops_a;
     o << "  }\n";
@@ -815,16 +829,19 @@ bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
   const uint64_t pk = ceil_pow2(k);
   if (!(pk > C || (pk == C && k <= m))) return false;
   if ((k + C - 1) / C > kMaxChunks) return false;
-  if (shard_bytes == 0 || shard_bytes % kUnitBytes) return false;
+  if (shard_bytes != 1024 && (shard_bytes == 0 || shard_bytes % kUnitBytes)) return false;
   return k * shard_bytes + 4096 < 0x80000000ull && m * shard_bytes + 4096 < 0x80000000ull;
 }
+
+uint32_t pieces(uint64_t shard_bytes) { return shard_bytes == 1024 ? 2u : 1u; }
 
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft:p" + std::to_string(prefetch_of(s)) + "n" + std::to_string(nt_of()) + "s" +
                   std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 1)) +
                   "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + ":" + std::to_string(s.k) + ":" +
-                  std::to_string(s.m) + ":" + std::to_string(s.flags) + ":";
+                  std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
+                  (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "");
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
   k.push_back(':');
   for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));
@@ -883,7 +900,7 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st) {
   if (n_stripes == 0) return hipSuccess;
-  if (!supports(s.k, s.m, sb)) return hipErrorInvalidValue;
+  if (!supports(s.k, s.m, sb) || pieces(sb) != s.pieces) return hipErrorInvalidValue;
   const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));
   static std::mutex mu;
   static std::map<int, int> cus;
@@ -900,15 +917,16 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
       n_cu = it->second;
     }
   }
-  uint32_t ups = static_cast<uint32_t>(sb / kUnitBytes);
-  uint64_t n_units = n_stripes * ups;
+  uint32_t ups = s.pieces > 1 ? 1u : static_cast<uint32_t>(sb / kUnitBytes);
+  uint64_t n_units = s.pieces > 1 ? (n_stripes + 1) / 2 : n_stripes * ups;
+  uint64_t n_st = n_stripes;
   // one workgroup per CU (128 KiB of LDS for chunk 64), persistent over the units
   const uint32_t per_cu = C == 64 ? 1 : 2;
   const uint64_t grid = std::min<uint64_t>(n_units, static_cast<uint64_t>(n_cu) * per_cu);
   uint32_t sb32 = static_cast<uint32_t>(sb);
   const unsigned char *d = data, *r = rec ? rec : data;
   unsigned char *o = out;
-  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units};
+  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st};
   return hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(grid), 1, 1, (C / 8) * 64, 1, 1, 0, st, args, nullptr);
 }
 

@@ -45,14 +45,17 @@ struct Spec {
   std::vector<uint8_t> skip;      // k entries (or empty): data shard read as zero (erased)
   std::vector<uint8_t> out_mode;  // m entries (or empty = all kOutStore)
   int prefetch = -1;              // next-chunk positions loaded early (-1: RS_AMD_FFT_PREFETCH, default 4)
+  uint32_t pieces = 1;            // stripes per 2 KiB unit: 1, or 2 for 1 KiB shards (pieces())
 };
 
 constexpr uint64_t kUnitBytes = 2048;  // shard bytes one workgroup covers per unit
 
 // chunk 32 or 64, high rate, at most kMaxChunks IFFT chunks (code size), shards of
-// whole 2 KiB units with k * shard_bytes below 2 GiB (32-bit buffer offsets)
+// whole 2 KiB units (or 1 KiB: a unit spans two stripes) with k * shard_bytes below
+// 2 GiB (32-bit buffer offsets)
 constexpr uint32_t kMaxChunks = 16;
 bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes);
+uint32_t pieces(uint64_t shard_bytes);  // Spec::pieces for a shard size
 
 std::string generate(const Spec &s, const std::string &name);
 std::string cache_key(const Spec &s);

@@ -71,7 +71,7 @@ def test_validation_precedes_device():
     with pytest.raises(R.InvalidShardSize):
         R.Encoder(10, 4, 0)
     with pytest.raises(R.LowRateUnsupported):
-        R.Encoder(2, 100, 64)  # low rate beyond 64 recovery shards (the reference panics on any)
+        R.Encoder(200, 400, 64)  # low-rate map past k * m = 65536 (the reference panics on any low rate)
     R.Encoder(10, 4, 66).deinit()  # tails accepted (root.zig:338-348 layout; the reference panics)
     with pytest.raises(R.TooFewOriginalShards):
         R.encode(10, 4, [])

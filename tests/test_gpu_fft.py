@@ -62,3 +62,42 @@ def test_fft_encode_c4_full(oracle):
     got = enc(k, m, data)
     exp = oracle.encode_batch(k, m, data, threads=16)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("k,m", [(32, 32), (64, 64), (200, 55), (33, 17), (100, 20)])
+@pytest.mark.parametrize("n", [1, 2, 7])
+def test_fft_encode_1k_shards(oracle, k, m, n):
+    """1 KiB shards (the reference harness size, benchmarks.zig:11): a unit spans two
+    stripes; an odd batch's last unit has no second stripe (zero-record resource:
+    nothing read or written past the batch — a guard stripe stays untouched)."""
+    sb = 1024
+    rng = np.random.default_rng(k * 31 + m + n)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    assert "fft_encode" in R.encode_kernel_name(k, m, sb)
+    d = torch.from_numpy(data).to(DEV)
+    p = torch.full((n + 1, m, sb), 7, dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p[:n])
+    torch.cuda.synchronize()
+    got = p.cpu().numpy()
+    assert np.array_equal(got[:n], oracle.encode_batch(k, m, data, threads=8))
+    assert (got[n] == 7).all()
+
+
+def test_fft_syndrome_1k_shards(oracle, monkeypatch):
+    """RS(200,55) losing 40 data shards at 1 KiB: syndromes on the two-stripe FFT variant."""
+    monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")
+    k, m, sb, n = 200, 55, 1024, 5
+    rng = np.random.default_rng(2055)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=8)
+    present = np.ones(k + m, np.uint8)
+    lost = list(range(3, 200, 5))[:40]
+    present[lost] = 0
+    assert "syndrome+net_fft_encode" in R.reconstruct_kernel_name(k, m, sb, present)
+    d = torch.from_numpy(data).to(DEV)
+    d[:, lost] = 0
+    pr = torch.from_numpy(par).to(DEV)
+    out = torch.zeros((n, len(lost), sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, d, pr, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), data[:, lost])

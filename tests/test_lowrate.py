@@ -16,6 +16,8 @@ import pytest
 from rs_amd import reedsol_amd as R
 
 LOW_KM = [(1, 2), (2, 4), (3, 5), (3, 6), (5, 9), (4, 16), (10, 20), (7, 40), (16, 64)]
+# past 64 recovery shards: maps in passes of <= 64 outputs (rs_capi.cpp MapPlan)
+LOW_KM_WIDE = [(2, 100), (10, 200), (3, 1000), (17, 130), (100, 600)]
 
 
 def gf2_rank(rows):
@@ -72,8 +74,14 @@ def test_low_rate_network_compiles(k, m):
 
 
 def test_low_rate_limits(monkeypatch):
+    R.Encoder(2, 100, 64)
+    R.Encoder(100, 600, 64)
+    with pytest.raises(R.LowRateUnsupported):  # k * m > 65536
+        R.Encoder(200, 400, 64)
     with pytest.raises(R.LowRateUnsupported):
-        R.Encoder(2, 100, 64)
+        R.Encoder(16, 4097, 64)
+    assert R.encode_kernel_name(2, 100, 1 << 16) == "net_encode_low_i2_o100"
+    assert R.encode_kernel_name(100, 600, 1 << 16) == "lowrate_matrix"  # 100 x 64 per pass: past the network cap
     assert R.encode_kernel_name(10, 20, 1 << 16) == "net_encode_low_i10_o20"
     # 256 blocks: a background-compiled network (table matrix kernel until it is ready)
     assert R.encode_kernel_name(16, 64, 1 << 16) == "net_encode_low_i16_o64"
@@ -88,11 +96,12 @@ gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
 
 @pytest.mark.gpu
 @gpu
-@pytest.mark.parametrize("k,m", LOW_KM)
+@pytest.mark.parametrize("k,m", LOW_KM + LOW_KM_WIDE)
 @pytest.mark.parametrize("jit", ["1", "0"])
 @pytest.mark.parametrize("sb", [192, 8192])
 def test_low_rate_gpu_vs_oracle_and_roundtrip(oracle, monkeypatch, k, m, jit, sb):
     monkeypatch.setenv("RS_AMD_JIT", jit)
+    monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")  # every pass's network, not the table kernels of a pending compile
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(k * 97 + m + sb)
     n = 3
