@@ -25,6 +25,7 @@
 #include "rs_internal.hpp"
 #include "rs_fftnet.hpp"
 #include "rs_jit.hpp"
+#include "rs_psyn.hpp"
 
 using namespace rs;
 
@@ -211,6 +212,7 @@ struct DecodePlan {
   bool syndrome = false;
   std::shared_ptr<DevBuf> skip;  // k-bit mask of the erased data shards
   std::shared_ptr<FftSlot> syn_fft;  // the syndromes' encode on the bit-sliced FFT kernel (wide codes)
+  std::shared_ptr<FftSlot> inv_fft;  // every original lost, k == m == chunk: the encode inverted
 };
 
 // Compile (once) and return the plan's network kernel; nullptr if hipRTC failed
@@ -591,6 +593,17 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   plan->work = static_cast<uint32_t>(W);
   plan->chunk = static_cast<uint32_t>(C);
   plan->trunc = static_cast<uint32_t>(end);
+  // every original lost and every recovery shard present, k == m == chunk: the data are
+  // FFT_C(IFFT_0(recovery)) (rs_fftnet.hpp Spec::inverse); the plan's other kernels stay
+  // the fallback
+  if (e == k && present_count == m && (mode == "auto" || mode == "net") && fft_enabled() &&
+      fftnet::supports_inverse(k, m, sb)) {
+    plan->inv_fft = std::make_shared<FftSlot>();
+    plan->inv_fft->spec.k = static_cast<uint32_t>(k);
+    plan->inv_fft->spec.m = static_cast<uint32_t>(m);
+    plan->inv_fft->spec.flags = flags;
+    plan->inv_fft->spec.inverse = true;
+  }
 
   if (use_matrix) {
     jit::NetSpec map;
@@ -1088,6 +1101,8 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
     return "lowrate_matrix";
   }
   const std::string mode = decode_mode_env();
+  if (e == k && have == m && (mode == "auto" || mode == "net") && fft_enabled() && fftnet::supports_inverse(k, m, sb))
+    return net_name("fft_inverse", m, k);
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
     return net_name("reconstruct", k, e);
@@ -1126,6 +1141,34 @@ int rs_net_wait(void) {
   });
 }
 
+int rs_psyn_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compile_ms, uint64_t *code_bytes) {
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, jit::kUnitBytes);
+    if (st) return st;
+    if (is_low_rate(k, m) || (flags & RS_FLAG_QUIRK_D1) || !psyn::supports(k, m, jit::kUnitBytes))
+      return fail(RS_ERR_INVALID_ARGUMENT, "no per-stripe syndrome network for this code");
+    jit::NetSpec map;
+    encode_map(k, m, flags & RS_FLAG_QUIRK_D2, map);
+    psyn::Spec spec;
+    spec.k = static_cast<uint32_t>(k);
+    spec.m = static_cast<uint32_t>(m);
+    spec.flags = flags & RS_FLAG_QUIRK_D2;
+    spec.images = std::move(map.images);
+    spec.cantor.assign(cantor_basis(), cantor_basis() + 16);
+    std::string err;
+    size_t bytes = 0;
+    if (!psyn::compile_check(spec, err, compile_ms, &bytes)) return fail(RS_ERR_DEVICE, err);
+    if (code_bytes) *code_bytes = bytes;
+    return RS_OK;
+  });
+}
+
+// RS_AMD_FFT_CHECK_INVERSE=1: the checks below take the inverse form (k == m == chunk)
+static bool check_inverse(uint64_t k, uint64_t m) {
+  const char *e = std::getenv("RS_AMD_FFT_CHECK_INVERSE");
+  return e && std::strcmp(e, "1") == 0 && fftnet::supports_inverse(k, m, fftnet::kUnitBytes);
+}
+
 int rs_fft_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compile_ms, uint64_t *code_bytes,
                          uint64_t *valu_ops) {
   return guarded([&]() -> int {
@@ -1138,6 +1181,7 @@ int rs_fft_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compile
     spec.flags = flags;
     // RS_AMD_FFT_CHECK_PIECES=2: the 1 KiB-shard variant (units of two stripes)
     if (const char *pc = std::getenv("RS_AMD_FFT_CHECK_PIECES")) spec.pieces = std::strcmp(pc, "2") == 0 ? 2 : 1;
+    spec.inverse = check_inverse(k, m);
     if (valu_ops) {
       const fftnet::Stats s = fftnet::stats(spec);
       *valu_ops = s.ops_a + s.ops_b + s.ops_io;
@@ -1160,6 +1204,7 @@ int rs_fft_selftest(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *skip,
     spec.m = static_cast<uint32_t>(m);
     spec.flags = flags;
     if (skip) spec.skip.assign(skip, skip + k);
+    spec.inverse = check_inverse(k, m);
     const uint64_t bad = fftnet::selftest(spec, trials);
     if (mismatches) *mismatches = bad;
     return RS_OK;
@@ -1332,6 +1377,15 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     }
     std::shared_ptr<DecodePlan> plan;
     if ((st = get_decode_plan(dev, k, m, sb, flags, present, plan))) return st;
+    if (plan->inv_fft && max_nv == 4) {
+      const fftnet::Spec *fs = nullptr;
+      if (const jit::Kernel *fk = fft_kernel(*plan->inv_fft, sb, &fs)) {
+        HIP_TRY(fftnet::launch(*fk, *fs, static_cast<const uint8_t *>(d_recovery), rec_stride, nullptr, 0,
+                               static_cast<uint8_t *>(d_restored), out_stride, sb, n_stripes,
+                               static_cast<hipStream_t>(stream)));
+        return RS_OK;
+      }
+    }
     if (plan->net && !plan->syndrome && max_nv == 4) {
       if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,
@@ -1509,6 +1563,65 @@ int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &o
   return RS_OK;
 }
 
+// Per code (k, m, flags): the syndrome-network kernel of rs_psyn.hpp and the code's
+// encode coefficients G [m][k] in HBM (for the per-stripe plans).
+struct PsynPlan {
+  std::mutex mu;
+  bool failed = false;
+  psyn::Spec spec;
+  std::shared_ptr<DevBuf> G;
+};
+std::map<std::string, std::shared_ptr<PsynPlan>> g_psyn_plans;
+
+int psyn_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<PsynPlan> &out) {
+  const std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                          std::to_string(flags & RS_FLAG_QUIRK_D2);
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto it = g_psyn_plans.find(key);
+    if (it != g_psyn_plans.end()) {
+      out = it->second;
+      return RS_OK;
+    }
+  }
+  auto p = std::make_shared<PsynPlan>();
+  jit::NetSpec map;
+  encode_map(k, m, flags & RS_FLAG_QUIRK_D2, map);
+  std::vector<uint16_t> G(m * k + 16);  // coefficients, then the Cantor basis (launch_psyn_plan)
+  for (uint64_t t = 0; t < k; t++)
+    for (uint64_t r = 0; r < m; r++) G[r * k + t] = map.images[(t * m + r) * 16];  // image of 1 = the coefficient
+  std::copy(cantor_basis(), cantor_basis() + 16, G.begin() + m * k);
+  p->spec.cantor.assign(cantor_basis(), cantor_basis() + 16);
+  int st = upload(G.data(), G.size() * sizeof(uint16_t), dev, p->G);
+  if (st) return st;
+  p->spec.k = static_cast<uint32_t>(k);
+  p->spec.m = static_cast<uint32_t>(m);
+  p->spec.flags = flags & RS_FLAG_QUIRK_D2;
+  p->spec.images = std::move(map.images);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_psyn_plans.emplace(key, p).first->second;
+  return RS_OK;
+}
+
+const jit::Kernel *psyn_kernel(PsynPlan &p) {
+  std::lock_guard<std::mutex> lk(p.mu);
+  if (p.failed) return nullptr;
+  std::string err;
+  const jit::Kernel *k = psyn::get(p.spec, err);
+  if (!k) {
+    p.failed = true;
+    warn_once_per_reason("[rs_amd] per-stripe syndrome network unavailable, using table kernels: ", err);
+  }
+  return k;
+}
+
+bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
+  const char *pm = std::getenv("RS_AMD_PATTERNS");
+  const std::string mode = pm ? pm : "";
+  return !(flags & RS_FLAG_QUIRK_D1) && (mode.empty() || mode == "auto" || mode == "psyn") && jit::enabled() &&
+         psyn::supports(k, m, sb);
+}
+
 }  // namespace
 
 int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const uint8_t *d_present,
@@ -1536,6 +1649,29 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
     const uint16_t *dexp, *dlog, *dlw;
     if ((st = device_tables(dev, &dexp, &dlog, &dlw))) return st;
+    // syndrome network (rs_psyn.hpp): the code's fixed k -> m network plus a per-stripe
+    // e x e solve; corrected multiply, k <= 64, m <= 4, whole 4 KiB units
+    if (max_nv == 4 && psyn_enabled(k, m, sb, flags)) {
+      std::shared_ptr<PsynPlan> pp;
+      if ((st = psyn_plan(dev, k, m, flags, pp))) return st;
+      if (const jit::Kernel *pk = psyn_kernel(*pp)) {
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const uint32_t mo = psyn::max_out(static_cast<uint32_t>(k), static_cast<uint32_t>(m));
+        const uint32_t pdw = psyn::plan_dwords(static_cast<uint32_t>(k), static_cast<uint32_t>(m));
+        void *blk = nullptr;
+        HIP_TRY(hipMallocAsync(&blk, n_stripes * pdw * sizeof(uint32_t), s));
+        hipError_t e = launch_psyn_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m), mo,
+                                        max_e, n_stripes, static_cast<const uint16_t *>(pp->G->p), dexp, dlog,
+                                        static_cast<uint32_t *>(blk), pdw, d_status, s);
+        if (e == hipSuccess)
+          e = psyn::launch(*pk, pp->spec, static_cast<const uint8_t *>(d_original), orig_stride,
+                           static_cast<const uint8_t *>(d_recovery), rec_stride, static_cast<uint8_t *>(d_restored),
+                           out_stride, sb, n_stripes, static_cast<const uint32_t *>(blk), s);
+        (void)hipFreeAsync(blk, s);
+        if (e != hipSuccess) return hip_fail(e, "per-stripe syndrome network");
+        return RS_OK;
+      }
+    }
     std::shared_ptr<DevBuf> tw;
     size_t off_fft = 0;
     if ((st = twiddle_plan(dev, W, flags, tw, off_fft))) return st;

@@ -190,9 +190,12 @@ Plan make_plan(const Spec &s) {
   p.WB = p.n - 3;
   p.NW = 1u << p.WB;
   p.d1 = (s.flags & RS_FLAG_QUIRK_D1) != 0;
-  p.truncs = encode_chunk_truncs(s.k, s.m, (s.flags & RS_FLAG_QUIRK_D2) != 0);
+  // inverse: parity = FFT_0(IFFT_C(data)) for k == m == C (no truncation, D2 cannot
+  // drop the only chunk), so data = FFT_C(IFFT_0(parity)): each butterfly layer of one
+  // skew undoes the other's (Generic.zig:15-147), under either multiply
+  p.truncs = s.inverse ? std::vector<uint64_t>{p.C} : encode_chunk_truncs(s.k, s.m, (s.flags & RS_FLAG_QUIRK_D2) != 0);
   for (size_t j = 0; j < p.truncs.size(); j++) {
-    p.ifft.push_back(ifft_layers(p.C, p.truncs[j], (j + 1) * p.C));  // root.zig:143-166
+    p.ifft.push_back(ifft_layers(p.C, p.truncs[j], s.inverse ? 0 : (j + 1) * p.C));  // root.zig:143-166
     std::vector<uint8_t> v(p.C, 0);
     for (uint32_t q = 0; q < p.C; q++) {
       const uint64_t g = j * p.C + q;
@@ -200,7 +203,7 @@ Plan make_plan(const Spec &s) {
     }
     p.valid.push_back(std::move(v));
   }
-  p.fft = fft_layers(p.C, s.m, 0);  // root.zig:169
+  p.fft = fft_layers(p.C, s.inverse ? s.k : s.m, s.inverse ? p.C : 0);  // root.zig:169
   p.out_mode.assign(p.C, kOutNone);
   for (uint32_t q = 0; q < s.m; q++) p.out_mode[q] = s.out_mode.empty() ? kOutStore : s.out_mode[q];
   return p;
@@ -272,6 +275,7 @@ int env_int(const char *name, int def) {
 }
 
 int nt_of() { return env_int("RS_AMD_FFT_NT", 3) & 3; }
+bool blocked_of() { return env_int("RS_AMD_FFT_BLOCKED", 0) != 0; }
 
 int prefetch_of(const Spec &s) {
   return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", 4)));
@@ -509,6 +513,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // RS_AMD_FFT_NT: non-temporal loads (bit 0) / stores (bit 1) (cache policy bit nt = 2);
   // default both: RS(200,55) 256 KiB encode 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
   const int nt = nt_of();
+  const bool blocked = blocked_of();
   o << "#define RS_AUX_LD " << ((nt & 1) ? 2 : 0) << "\n#define RS_AUX_ST " << ((nt & 2) ? 2 : 0) << "\n" << kPrelude;
   // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
@@ -539,19 +544,28 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
        "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
-       // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division)
-       "  u64 stripe = blockIdx.x / ups;\n"
-       "  u32 uu = blockIdx.x - (u32)stripe * ups;\n"
-       "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n"
+       // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division in the loop);
+       // RS_AMD_FFT_BLOCKED: workgroup b takes the contiguous units [b * per, b * per + per)
+       << (blocked ? "  const u64 per = (n_units + gridDim.x - 1) / gridDim.x, ub = blockIdx.x * per,\n"
+                     "            ue = ub + per < n_units ? ub + per : n_units;\n"
+                     "  u64 stripe = ub / ups;\n"
+                     "  u32 uu = (u32)(ub - stripe * ups);\n"
+                     "  const u32 gdiv = 0u, gmod = 1u;\n"
+                   : "  const u64 ub = blockIdx.x, ue = n_units;\n"
+                     "  u64 stripe = blockIdx.x / ups;\n"
+                     "  u32 uu = blockIdx.x - (u32)stripe * ups;\n"
+                     "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n")
+    << 
        "  const __amdgpu_buffer_rsrc_t RZ = __builtin_amdgcn_make_buffer_rsrc((void *)data, (short)0, 0, 0x00020000);\n"
        "  v4 la0[8], lb0[8];\n"
        "  {  // prologue: the first unit's leading positions of chunk 0\n"
        "  const u32 sbl = sb, uo = uu * 2048u + loff, uo1 = " << half << ";\n";
-  rsrc_pair(o, "RD", "data", "ds", "stripe", s.k, "blockIdx.x < n_units");
+  rsrc_pair(o, "RD", "data", "ds", "stripe", s.k, "ub < ue");
   // (loads emitted below, once emit_loads exists)
   std::ostringstream hdr2;
   hdr2 << "#pragma unroll 1\n"
-       "  for (u64 u = blockIdx.x; u < n_units; u += gridDim.x) {\n"
+    << (blocked ? "  for (u64 u = ub; u < ue; u++) {\n" : "  for (u64 u = ub; u < ue; u += gridDim.x) {\n")
+    << 
        "  u32 sbl = sb;\n"
        "  asm volatile(\"\" : \"+s\"(sbl));  // shard offsets are recomputed per unit (SALU), not hoisted into VGPRs\n"
        "  const u32 uo = uu * 2048u + loff, uo1 = " << half << ";\n";
@@ -748,7 +762,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   o << "  u64 stripe_n = stripe + gdiv;\n  u32 uu_n = uu + gmod;\n  if (uu_n >= ups) { uu_n -= ups; stripe_n++; }\n";
   if (pf && xunit) {
     o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = " << (two ? "loff" : "uon + 1024u") << ";\n";
-    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, "u + gridDim.x < n_units");
+    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, blocked ? "u + 1u < ue" : "u + gridDim.x < ue");
     emit_loads(0, 0, pf, "RDn", "uon", "uon1");
     o << "  }\n";
   }
@@ -835,13 +849,18 @@ bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 
 uint32_t pieces(uint64_t shard_bytes) { return shard_bytes == 1024 ? 2u : 1u; }
 
+bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
+  return k == m && ceil_pow2(m) == m && supports(k, m, shard_bytes);
+}
+
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft:p" + std::to_string(prefetch_of(s)) + "n" + std::to_string(nt_of()) + "s" +
                   std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 1)) +
-                  "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + ":" + std::to_string(s.k) + ":" +
+                  "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + "b" + std::to_string(blocked_of()) + ":" +
+                  std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
-                  (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "");
+                  (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "");
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
   k.push_back(':');
   for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));
@@ -852,7 +871,8 @@ std::string kernel_name(const Spec &s) {
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : cache_key(s)) h = (h ^ c) * 1099511628211ull;
   char name[96];
-  std::snprintf(name, sizeof name, "rs_fft_encode_k%u_m%u_%016llx", s.k, s.m, static_cast<unsigned long long>(h));
+  std::snprintf(name, sizeof name, "rs_fft_%s_k%u_m%u_%016llx", s.inverse ? "inverse" : "encode", s.k, s.m,
+                static_cast<unsigned long long>(h));
   return name;
 }
 
@@ -900,7 +920,8 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st) {
   if (n_stripes == 0) return hipSuccess;
-  if (!supports(s.k, s.m, sb) || pieces(sb) != s.pieces) return hipErrorInvalidValue;
+  if (!supports(s.k, s.m, sb) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
+    return hipErrorInvalidValue;
   const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));
   static std::mutex mu;
   static std::map<int, int> cus;
@@ -975,6 +996,13 @@ uint64_t selftest(const Spec &s, int trials) {
       for (uint32_t q = 0; q < C; q++) acc[q] ^= v[q];
     }
     for (const Layer &L : P.fft) apply(acc, L);
+    if (s.inverse) {  // the kernel's output is data whose encode gives back `in`
+      std::vector<uint16_t> data(s.k), par(s.m);
+      for (uint32_t q = 0; q < s.k; q++) data[q] = to_uv(acc[q]);
+      scalar_encode(data.data(), s.k, s.m, P.d1, (s.flags & RS_FLAG_QUIRK_D2) != 0, par.data());
+      for (uint32_t q = 0; q < s.m; q++) bad += par[q] != in[q];
+      continue;
+    }
     for (uint32_t q = 0; q < s.m; q++) bad += to_uv(acc[q]) != ref[q];
   }
   return bad;

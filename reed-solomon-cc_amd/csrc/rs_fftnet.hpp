@@ -46,7 +46,13 @@ struct Spec {
   std::vector<uint8_t> out_mode;  // m entries (or empty = all kOutStore)
   int prefetch = -1;              // next-chunk positions loaded early (-1: RS_AMD_FFT_PREFETCH, default 4)
   uint32_t pieces = 1;            // stripes per 2 KiB unit: 1, or 2 for 1 KiB shards (pieces())
+  // the encode inverted (k == m == chunk): input = the m recovery shards, IFFT at skew 0,
+  // FFT at skew chunk, output = the k originals (reconstruct with every original lost)
+  bool inverse = false;
 };
+
+// the inverse form exists for this code (single full chunk: k == m == chunk)
+bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes);
 
 constexpr uint64_t kUnitBytes = 2048;  // shard bytes one workgroup covers per unit
 

@@ -65,6 +65,8 @@ void build(Tables &t) {
 
 }  // namespace
 
+const uint16_t *cantor_basis() { return kCantor; }
+
 const Tables &tables() {
   std::call_once(g_once, [] {
     g_tables.reset(new Tables);

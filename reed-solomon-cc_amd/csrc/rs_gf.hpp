@@ -44,6 +44,9 @@ struct Tables {
 };
 
 const Tables &tables();  // built once, thread-safe
+// the Cantor basis (gf.zig:8-13) in polynomial form: a symbol v is the element
+// XOR of cantor_basis()[i] over its set bits i (polynomial 0x1002D coordinates)
+const uint16_t *cantor_basis();
 
 inline uint16_t add_mod(uint32_t x, uint32_t y) {  // utilities.zig:10-13
   uint32_t s = x + y;

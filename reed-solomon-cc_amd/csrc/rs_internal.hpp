@@ -125,6 +125,14 @@ hipError_t launch_pattern_matrix(const uint8_t *d_present, uint64_t present_stri
                                  const RsTab *tab_fft, const uint16_t *d_exp, const uint16_t *d_log, uint16_t *images,
                                  RsTab *tabs, int32_t *srcs, int32_t *nout, hipStream_t s);
 
+// Per-stripe plan of the syndrome-network path (rs_psyn.hpp): G [m][k] encode
+// coefficients then the 16 Cantor basis elements (polynomial form); plan
+// [n][plan_dw] (k <= 64, m <= kPsynMaxM, max_out <= m)
+constexpr uint32_t kPsynMaxM = 8;
+hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_out,
+                            uint32_t max_e, uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log,
+                            uint32_t *plan, uint32_t plan_dw, int32_t *status, hipStream_t s);
+
 // present rows trimmed to the k shards the matrix path decodes from (out: [n][k+m])
 hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
                                uint8_t *out, hipStream_t s);

@@ -276,6 +276,11 @@ std::string tuning_key(const Tuning &t) {
 
 }  // namespace
 
+const char *net_prelude() { return kPrelude; }
+void emit_network_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::vector<bool> &init, int t) {
+  emit_input(o, rows, init, t);
+}
+
 uint64_t max_blocks() {
   const int v = env_int("RS_AMD_NET_MAX_BLOCKS", 0);
   return v > 0 ? static_cast<uint64_t>(v) : kMaxBlocks;

@@ -17,6 +17,7 @@
 
 #include <cstdint>
 #include <functional>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -65,6 +66,13 @@ bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes);
 
 // CUDA-style source of the kernel `name` (exposed for tests / inspection).
 std::string generate(const NetSpec &spec, const std::string &name);
+
+// Building blocks for other generated kernels: the device prelude (tr8 / ld / planes /
+// st over a wave's 4 KiB unit; RS_NT must be defined first), and one input's
+// Four-Russians XOR network into accumulators a<r> (rows[r] = 16-bit mask of the
+// input planes feeding accumulator r; `init`: accumulators already assigned).
+const char *net_prelude();
+void emit_network_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::vector<bool> &init, int t);
 
 struct Kernel {
   hipModule_t module = nullptr;

@@ -1189,6 +1189,76 @@ __global__ __launch_bounds__(256) void k_pattern_images(const uint8_t *__restric
   for (; j < max_e; j++) img[j * 16] = 0;
 }
 
+// Per-stripe plan of the syndrome-network path (rs_psyn.hpp), one thread per stripe:
+// E = the erased originals, R = the first e present recovery rows, A = G[R][E] (e x e
+// block of the code's encode coefficients, G[r][t] = parity r of data t = 1), and
+// x_E = A^-1 s_R with s_r = p_r ^ Enc_r(data, erased read as 0). Block per stripe
+// (u32): [0..1] erased mask, [2] R mask, [3] outputs stored = min(e, max_e) (0: none),
+// then [4 + r * max_out + j] = A^-1[j][i(r)] in polynomial coordinates (bit i: the
+// coefficient of alpha^i; 0 for rows outside R), the form the kernel multiplies in.
+// G: [m][k] coefficients followed by the 16 Cantor basis elements (polynomial form).
+__device__ __forceinline__ uint32_t gf_mul_d(uint32_t a, uint32_t b, const uint16_t *exp, const uint16_t *log) {
+  return (a == 0 || b == 0) ? 0u : exp[add_mod_d(log[a], log[b])];
+}
+
+__global__ __launch_bounds__(64) void k_psyn_plan(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                  uint32_t k, uint32_t m, uint32_t max_out, uint32_t max_e, uint64_t n,
+                                                  const uint16_t *__restrict__ G, const uint16_t *__restrict__ exp,
+                                                  const uint16_t *__restrict__ log, uint32_t *__restrict__ plan,
+                                                  uint32_t plan_dw, int32_t *__restrict__ status) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint8_t *pr = present + s * present_stride;
+  uint32_t *pl = plan + s * plan_dw;
+  uint32_t have = 0, e = 0;
+  for (uint32_t i = 0; i < k + m; i++) have += pr[i] ? 1 : 0;
+  for (uint32_t i = 0; i < k; i++) e += pr[i] ? 0 : 1;
+  if (status) status[s] = have < k ? 2 : (e > max_e ? 14 : 0);  // as k_pattern_tables
+  pl[0] = pl[1] = pl[2] = pl[3] = 0;
+  if (have < k || e == 0) return;  // nothing restored (e <= present recovery <= m from here)
+  uint32_t E[kPsynMaxM], R[kPsynMaxM], em[2] = {0, 0}, rm = 0;
+  for (uint32_t i = 0, c = 0; i < k && c < e; i++)
+    if (!pr[i]) E[c++] = i, em[i / 32] |= 1u << (i % 32);
+  for (uint32_t r = 0, c = 0; r < m && c < e; r++)
+    if (pr[k + r]) R[c++] = r, rm |= 1u << r;
+  // Gauss-Jordan on [A | I] over GF(2^16)
+  uint32_t A[kPsynMaxM][2 * kPsynMaxM];
+  for (uint32_t i = 0; i < e; i++)
+    for (uint32_t j = 0; j < 2 * e; j++) A[i][j] = j < e ? G[R[i] * k + E[j]] : (j - e == i ? 1u : 0u);
+  for (uint32_t c = 0; c < e; c++) {
+    uint32_t piv = c;
+    while (piv < e && A[piv][c] == 0) piv++;
+    if (piv == e) return;  // singular: cannot happen for an MDS code (nothing restored)
+    for (uint32_t j = 0; j < 2 * e; j++) {
+      const uint32_t t = A[c][j];
+      A[c][j] = A[piv][j];
+      A[piv][j] = t;
+    }
+    const uint32_t inv = exp[(65535u - log[A[c][c]]) % 65535u];
+    for (uint32_t j = 0; j < 2 * e; j++) A[c][j] = gf_mul_d(A[c][j], inv, exp, log);
+    for (uint32_t i = 0; i < e; i++)
+      if (i != c && A[i][c]) {
+        const uint32_t f = A[i][c];
+        for (uint32_t j = 0; j < 2 * e; j++) A[i][j] ^= gf_mul_d(f, A[c][j], exp, log);
+      }
+  }
+  const uint16_t *cantor = G + m * k;
+  for (uint32_t r = 0; r < m; r++) {
+    int32_t ir = -1;
+    for (uint32_t i = 0; i < e; i++) ir = R[i] == r ? static_cast<int32_t>(i) : ir;
+    for (uint32_t j = 0; j < max_out; j++) {
+      const uint32_t c = (ir >= 0 && j < e) ? A[j][e + ir] : 0u;  // x_j += A^-1[j][i] s_{R_i}
+      uint32_t poly = 0;
+      for (int b = 0; b < 16; b++) poly ^= (c >> b & 1u) ? cantor[b] : 0u;
+      pl[4 + r * max_out + j] = poly;
+    }
+  }
+  pl[0] = em[0];
+  pl[1] = em[1];
+  pl[2] = rm;
+  pl[3] = e < max_e ? e : max_e;
+}
+
 // The matrix path decodes from exactly k received shards (the present originals and
 // the first e present recovery shards), so the erasure locator must be evaluated for
 // that set: present rows with the other recovery shards marked absent.
@@ -1599,6 +1669,16 @@ hipError_t launch_pattern_matrix(const uint8_t *d_present, uint64_t present_stri
                                  RsTab *tabs, int32_t *srcs, int32_t *nout, hipStream_t s) {
   return launch_pattern_matrix_impl(d_present, present_stride, k, m, C, W, n, max_e, logs, tab_ifft, tab_fft, d_exp,
                                     d_log, images, tabs, srcs, nout, s);
+}
+
+hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_out,
+                            uint32_t max_e, uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log,
+                            uint32_t *plan, uint32_t plan_dw, int32_t *status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (k > 64 || m > kPsynMaxM || max_out > m || plan_dw < 4 + m * max_out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_psyn_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present, present_stride,
+                     k, m, max_out, max_e, n, G, d_exp, d_log, plan, plan_dw, status);
+  return hipGetLastError();
 }
 
 hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,

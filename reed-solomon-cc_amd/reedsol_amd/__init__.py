@@ -90,6 +90,7 @@ def lib():
         "rs_net_wait": (C.c_int, []),
         "rs_jit_stats": (C.c_int, [vp, vp, vp]),
         "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
+        "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
         "rs_fft_selftest": (C.c_int, [u64, u64, u32, vp, C.c_int, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
@@ -357,6 +358,13 @@ def fft_compile_check(k, m, flags=0) -> dict:
     ms, b, ops = C.c_double(), C.c_uint64(), C.c_uint64()
     _check(lib().rs_fft_compile_check(k, m, flags, C.byref(ms), C.byref(b), C.byref(ops)))
     return {"compile_ms": ms.value, "code_bytes": b.value, "valu_ops_per_unit": ops.value}
+
+
+def psyn_compile_check(k, m, flags=0) -> dict:
+    """Generate + hipRTC-compile the per-stripe syndrome-network reconstruct kernel (no device)."""
+    ms, b = C.c_double(), C.c_uint64()
+    _check(lib().rs_psyn_compile_check(k, m, flags, C.byref(ms), C.byref(b)))
+    return {"compile_ms": ms.value, "code_bytes": b.value}
 
 
 def fft_selftest(k, m, flags=0, skip=None, trials=8) -> int:

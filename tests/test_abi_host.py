@@ -197,9 +197,36 @@ def test_fft_kernel_arithmetic(k, m, flags):
     assert R.fft_selftest(k, m, flags, skip=skip, trials=4) == 0
 
 
-def test_fft_kernel_compiles_for_gfx950():
+def test_fft_kernel_compiles_for_gfx950(monkeypatch):
     info = R.fft_compile_check(200, 55)
     assert info["code_bytes"] > 10000 and info["valu_ops_per_unit"] > 0
+    monkeypatch.setenv("RS_AMD_FFT_CHECK_PIECES", "2")  # 1 KiB shards: units of two stripes
+    assert R.fft_compile_check(32, 32)["code_bytes"] > 10000
+
+
+def test_psyn_kernel_compiles_for_gfx950():
+    """Per-stripe syndrome network (rs_psyn.hpp): generated and compiled per code; codes
+    outside its range (m > 4, D1 multiply, low rate) have none."""
+    assert R.psyn_compile_check(10, 4)["code_bytes"] > 10000
+    assert R.psyn_compile_check(4, 2, 2)["code_bytes"] > 1000
+    for k, m, flags in ((5, 5, 0), (10, 4, 1), (2, 4, 0)):
+        with pytest.raises(R.InvalidArgument):
+            R.psyn_compile_check(k, m, flags)
+
+
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("flags", [0, 3])
+def test_fft_inverse_arithmetic(monkeypatch, k, flags):
+    """Every original lost, RS(k,k) with k = chunk: the inverse FFT kernel's schedule
+    (IFFT at skew 0, FFT at skew chunk) yields data whose scalar encode is the input."""
+    monkeypatch.setenv("RS_AMD_FFT_CHECK_INVERSE", "1")
+    assert R.fft_selftest(k, k, flags, trials=6) == 0
+    present = np.ones(2 * k, np.uint8)
+    present[:k] = 0
+    assert R.reconstruct_kernel_name(k, k, 1024, present) == f"net_fft_inverse_i{k}_o{k}"
+    assert R.reconstruct_kernel_name(k, k, 1 << 20, present) == f"net_fft_inverse_i{k}_o{k}"
+    present[k] = 0  # a recovery shard lost too: not enough shards, no inverse form
+    assert R.reconstruct_kernel_name(k, k, 1024, present) != f"net_fft_inverse_i{k}_o{k}"
 
 
 def test_disk_code_object_cache(tmp_path):

@@ -415,13 +415,14 @@ def test_host_batch_error_drains_slices(oracle, monkeypatch, op):
 
 
 @pytest.mark.parametrize("k,m,sb", [(10, 4, 4096), (5, 5, 320), (4, 2, 2048), (16, 16, 1024), (20, 16, 512),
-                                    (200, 55, 512)])
+                                    (200, 55, 512), (4, 2, 8192), (3, 3, 4096), (64, 4, 4096), (7, 1, 4096)])
 @pytest.mark.parametrize("flags", [0, 1])
-@pytest.mark.parametrize("path", ["auto", "fft"])
+@pytest.mark.parametrize("path", ["auto", "matrix", "fft"])
 def test_reconstruct_per_stripe_patterns(oracle, monkeypatch, k, m, sb, flags, path):
-    """rs_reconstruct_batch_dev_patterns: erasure locator per stripe on the GPU (LDS FWHT),
-    then per-stripe matrices built on the GPU + the matrix kernel (auto, corrected, W <= 32,
-    max_e <= 8) or the FFT reconstruct kernels (RS_AMD_PATTERNS=fft)."""
+    """rs_reconstruct_batch_dev_patterns: the syndrome network (auto: corrected, k <= 64,
+    m <= 4, 4 KiB units; rs_psyn.hpp), else per-stripe matrices built on the GPU + the
+    matrix kernel (matrix: corrected, W <= 32, max_e <= 8), or the FFT reconstruct kernels
+    with the erasure locator evaluated per stripe (fft; the fallback of the others)."""
     monkeypatch.setenv("RS_AMD_PATTERNS", path)
     n = 9
     rng = np.random.default_rng(k * 31 + m + flags)
@@ -452,6 +453,32 @@ def test_reconstruct_per_stripe_patterns(oracle, monkeypatch, k, m, sb, flags, p
         assert (out[s, :len(missing)] == exp[0]).all(), (s, missing)
         if flags == 0:
             assert (out[s, :len(missing)] == data[s, missing]).all()
+
+
+@pytest.mark.parametrize("flags", [0, 2])
+@pytest.mark.parametrize("max_e", [1, 2, 4])
+def test_per_stripe_syndrome_network(oracle, flags, max_e):
+    """RS(10,4) 64 KiB, 4 random losses per stripe (the per-stripe benchmark's shape): the
+    syndrome network against the oracle, D2 schedule too; stripes losing more originals
+    than max_e restore the first max_e and report RS_ERR_INVALID_ARGUMENT (14)."""
+    k, m, sb, n = 10, 4, 65536, 37
+    rng = np.random.default_rng(1004 + flags + max_e)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n):
+        present[s, rng.choice(k + m, size=4, replace=False)] = 0
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    for s in range(n):
+        missing = [i for i in range(k) if not present[s, i]]
+        assert status[s] == (14 if len(missing) > max_e else 0), s
+        got = missing[:max_e]
+        assert (out[s, :len(got)] == data[s, got]).all(), (s, missing)
+        assert (out[s, len(got):] == 0xAB).all(), s
 
 
 @pytest.mark.parametrize("sb", [2, 6, 66, 70, 1000, 4102])

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-stripe erasure patterns (rs_reconstruct_batch_dev_patterns): RS(10,4) 1 MiB,
-random <= 4 erasures per stripe, matrix path vs FFT path (RS_AMD_PATTERNS)."""
+4 random erasures per stripe: syndrome network (auto) vs matrix vs FFT path (RS_AMD_PATTERNS)."""
 import json
 import os
 import sys
@@ -24,22 +24,30 @@ for s in range(n):
 dp = torch.from_numpy(present).to(dev)
 out = torch.empty((n, 4, sb), dtype=torch.uint8, device=dev)
 status = torch.empty((n,), dtype=torch.int32, device=dev)
-for path in ("fft", "auto", "fft", "auto"):
-    os.environ["RS_AMD_PATTERNS"] = path
+# extra variants: NAME=v1,v2 arguments after the stripe count (e.g. RS_AMD_PSYN_PF=1,2,3)
+variants = [("RS_AMD_PATTERNS", p) for p in ("matrix", "auto", "fft", "matrix", "auto")]
+for arg in sys.argv[2:]:
+    name, vals = arg.split("=")
+    variants += [(name, v) for v in vals.split(",")] * 2
+for var, val in variants:
+    os.environ[var] = val
+    path = os.environ.get("RS_AMD_PATTERNS", "auto")
     R.reconstruct_batch_dev_patterns(k, m, dp, data, par, out, status)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(3):
+    for _ in range(10):
         R.reconstruct_batch_dev_patterns(k, m, dp, data, par, out, status)
     b.record()
     torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / 3
+    ms = a.elapsed_time(b) / 10
     ok = True
     for s in range(0, n, max(1, n // 64)):
         miss = [i for i in range(k) if not present[s, i]]
         ok &= bool(torch.equal(out[s, :len(miss)], data[s, miss]))
     e_mean = float((present[:, :k] == 0).sum(1).mean())
     alg = n * sb * (k + e_mean)
-    print(json.dumps({"path": path, "stripes": n, "ms": round(ms, 3), "alg_TBps": round(alg / ms / 1e9, 3),
+    print(json.dumps({"path": path, var: val, "stripes": n, "ms": round(ms, 3), "alg_TBps": round(alg / ms / 1e9, 3),
                       "verified": ok}), flush=True)
+    if var != "RS_AMD_PATTERNS":
+        del os.environ[var]
