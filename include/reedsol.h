@@ -209,10 +209,11 @@ int rs_net_compile_check(uint64_t original_count, uint64_t recovery_count, const
  * loading it (a build check; no device needed). Optional outputs: compile time, code
  * object bytes, and the generated kernel's VALU instruction estimate per 2 KiB unit
  * (all waves). RS_ERR_INVALID_ARGUMENT if the code has no such kernel. */
-/* Generate the per-stripe syndrome-network reconstruct kernel (rs_psyn.hpp: the code's
- * fixed k -> m syndrome network plus the per-stripe e x e solve, used by
- * rs_reconstruct_batch_dev_patterns for k <= 64, m <= 4) and compile it with hipRTC
- * (no device). RS_ERR_INVALID_ARGUMENT if the code has no such kernel. */
+/* Generate the per-stripe syndrome-network reconstruct kernels of
+ * rs_reconstruct_batch_dev_patterns (rs_psyn.hpp) and compile them with hipRTC (no
+ * device): for k <= 64, m <= 4 the code's fixed k -> m syndrome network plus the
+ * per-stripe e x e solve; for wide codes (chunk 32 / 64) the FFT syndrome kernel with
+ * per-stripe masks plus the generic solve. RS_ERR_INVALID_ARGUMENT if the code has none. */
 int rs_psyn_compile_check(uint64_t original_count, uint64_t recovery_count, uint32_t flags, double *compile_ms,
                           uint64_t *code_bytes);
 int rs_fft_compile_check(uint64_t original_count, uint64_t recovery_count, uint32_t flags, double *compile_ms,

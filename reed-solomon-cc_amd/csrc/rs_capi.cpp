@@ -1145,8 +1145,26 @@ int rs_psyn_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compil
   return guarded([&]() -> int {
     int st = check_codec(k, m, jit::kUnitBytes);
     if (st) return st;
-    if (is_low_rate(k, m) || (flags & RS_FLAG_QUIRK_D1) || !psyn::supports(k, m, jit::kUnitBytes))
+    if (is_low_rate(k, m) || (flags & RS_FLAG_QUIRK_D1))
       return fail(RS_ERR_INVALID_ARGUMENT, "no per-stripe syndrome network for this code");
+    if (!psyn::supports(k, m, jit::kUnitBytes)) {
+      if (!fftnet::supports(k, m, jit::kUnitBytes))
+        return fail(RS_ERR_INVALID_ARGUMENT, "no per-stripe syndrome network for this code");
+      // wide code: the FFT syndrome kernel with per-stripe masks + the generic solve
+      fftnet::Spec fs;
+      fs.k = static_cast<uint32_t>(k);
+      fs.m = static_cast<uint32_t>(m);
+      fs.flags = flags & RS_FLAG_QUIRK_D2;
+      fs.dyn = true;
+      std::string err;
+      size_t b1 = 0, b2 = 0;
+      double t1 = 0, t2 = 0;
+      if (!fftnet::compile_check(fs, err, &t1, &b1)) return fail(RS_ERR_DEVICE, err);
+      if (!psyn::compile_check_solve(cantor_basis(), err, &t2, &b2)) return fail(RS_ERR_DEVICE, err);
+      if (compile_ms) *compile_ms = t1 + t2;
+      if (code_bytes) *code_bytes = b1 + b2;
+      return RS_OK;
+    }
     jit::NetSpec map;
     encode_map(k, m, flags & RS_FLAG_QUIRK_D2, map);
     psyn::Spec spec;
@@ -1615,6 +1633,38 @@ const jit::Kernel *psyn_kernel(PsynPlan &p) {
   return k;
 }
 
+// Wide codes: the FFT kernel with per-stripe masks for the syndromes + the generic solve
+struct WpsSlot {
+  std::shared_ptr<FftSlot> fft = std::make_shared<FftSlot>();
+  std::mutex mu;
+  bool solve_failed = false;
+};
+std::map<std::string, std::shared_ptr<WpsSlot>> g_wps;
+
+void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<WpsSlot> &out) {
+  const std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                          std::to_string(flags & RS_FLAG_QUIRK_D2);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto &p = g_wps[key];
+  if (!p) {
+    p = std::make_shared<WpsSlot>();
+    fftnet::Spec &fs = p->fft->spec;
+    fs.k = static_cast<uint32_t>(k);
+    fs.m = static_cast<uint32_t>(m);
+    fs.flags = flags & RS_FLAG_QUIRK_D2;
+    fs.dyn = true;
+  }
+  out = p;
+}
+
+bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t max_e) {
+  const char *pm = std::getenv("RS_AMD_PATTERNS");
+  const std::string mode = pm ? pm : "";
+  return !(flags & RS_FLAG_QUIRK_D1) && (mode.empty() || mode == "auto" || mode == "psyn") && fft_enabled() &&
+         fftnet::supports(k, m, sb) && fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
+         max_e <= psyn::kSolveMaxOut && m <= 64;
+}
+
 bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
@@ -1669,6 +1719,54 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
                            out_stride, sb, n_stripes, static_cast<const uint32_t *>(blk), s);
         (void)hipFreeAsync(blk, s);
         if (e != hipSuccess) return hip_fail(e, "per-stripe syndrome network");
+        return RS_OK;
+      }
+    }
+    // wide codes: syndromes on the FFT kernel (per-stripe masks), then the e x e solve
+    if (max_nv == 4 && wps_enabled(k, m, sb, flags, max_e)) {
+      std::shared_ptr<PsynPlan> pp;  // G and the Cantor basis
+      if ((st = psyn_plan(dev, k, m, flags, pp))) return st;
+      std::shared_ptr<WpsSlot> ws;
+      wps_slot(dev, k, m, flags, ws);
+      const fftnet::Spec *fs = nullptr;
+      const jit::Kernel *fk = fft_kernel(*ws->fft, sb, &fs);
+      const jit::Kernel *sk = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(ws->mu);
+        if (!ws->solve_failed) {
+          std::string err;
+          sk = psyn::get_solve(cantor_basis(), err);
+          if (!sk) {
+            ws->solve_failed = true;
+            warn_once_per_reason("[rs_amd] per-stripe solve kernel unavailable, using table kernels: ", err);
+          }
+        }
+      }
+      if (fk && sk) {
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const uint32_t dmw = fftnet::dyn_mask_words(*fs), pw = dmw + 2 + 64 + 64 * psyn::kSolveMaxOut;
+        const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (m * sb)));
+        void *blk = nullptr, *scratch = nullptr;
+        HIP_TRY(hipMallocAsync(&blk, n_stripes * pw * sizeof(uint32_t), s));
+        hipError_t e = hipMallocAsync(&scratch, per * m * sb, s);
+        if (e == hipSuccess)
+          e = launch_wps_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m), max_e,
+                              n_stripes, static_cast<const uint16_t *>(pp->G->p), dexp, dlog, static_cast<uint32_t *>(blk),
+                              pw, dmw, d_status, s);
+        for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += per) {
+          const uint64_t cnt = std::min(per, n_stripes - s0);
+          const uint32_t *bl = static_cast<const uint32_t *>(blk) + s0 * pw;
+          e = fftnet::launch(*fk, *fs, static_cast<const uint8_t *>(d_original) + s0 * orig_stride, orig_stride, nullptr,
+                             0, static_cast<uint8_t *>(scratch), m * sb, sb, cnt, s, bl, pw);
+          if (e == hipSuccess)
+            e = psyn::launch_solve(*sk, static_cast<const uint8_t *>(d_recovery) + s0 * rec_stride, rec_stride,
+                                   static_cast<const uint8_t *>(scratch), m * sb,
+                                   static_cast<uint8_t *>(d_restored) + s0 * out_stride, out_stride, sb, cnt, bl, pw,
+                                   dmw, s);
+        }
+        if (scratch) (void)hipFreeAsync(scratch, s);
+        (void)hipFreeAsync(blk, s);
+        if (e != hipSuccess) return hip_fail(e, "per-stripe wide-code reconstruct");
         return RS_OK;
       }
     }

@@ -499,6 +499,10 @@ std::string mask_expr(const std::vector<uint32_t> &per_wave) {
   return e;
 }
 
+// Spec::dyn mask block of a stripe (u32 words): bit p of words [0, dyn_store_word) =
+// data position p skipped (read as zero); bit q of the next 2 words = row q stored
+uint32_t dyn_store_word(const Plan &P) { return static_cast<uint32_t>((P.truncs.size() * P.C + 31) / 32); }
+
 std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   Plan P = make_plan(s);
   Gen g;
@@ -514,6 +518,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // default both: RS(200,55) 256 KiB encode 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
   const int nt = nt_of();
   const bool blocked = blocked_of();
+  const bool dyn = s.dyn;
   o << "#define RS_AUX_LD " << ((nt & 1) ? 2 : 0) << "\n#define RS_AUX_ST " << ((nt & 2) ? 2 : 0) << "\n" << kPrelude;
   // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
@@ -538,7 +543,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   const char *half = two ? "loff" : "uo + 1024u";  // offset of a unit's second KiB
   o << "extern \"C\" __global__ __launch_bounds__(" << NW * 64 << ") void " << name
     << "(const unsigned char *__restrict__ data, u64 ds, const unsigned char *__restrict__ rec, u64 rs,\n"
-       "    unsigned char *__restrict__ out, u64 os, u32 sb, u32 ups, u64 n_units, u64 n_st) {\n"
+       "    unsigned char *__restrict__ out, u64 os, u32 sb, u32 ups, u64 n_units, u64 n_st,\n"
+       "    const u32 *__restrict__ dm, u32 dmw) {\n"
     << "  __shared__ u32 xch[" << C * 8 * 64 << "];\n"
     << "  v4 *const xch4 = (v4 *)xch;\n"
     << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
@@ -561,6 +567,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
        "  {  // prologue: the first unit's leading positions of chunk 0\n"
        "  const u32 sbl = sb, uo = uu * 2048u + loff, uo1 = " << half << ";\n";
   rsrc_pair(o, "RD", "data", "ds", "stripe", s.k, "ub < ue");
+  // Spec::dyn: per-stripe masks (skipped data positions, stored rows) from dm
+  if (dyn) o << "  const u32 *DM = dm + (ub < ue ? stripe : 0ull) * dmw;\n";
   // (loads emitted below, once emit_loads exists)
   std::ostringstream hdr2;
   hdr2 << "#pragma unroll 1\n"
@@ -571,6 +579,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
        "  const u32 uo = uu * 2048u + loff, uo1 = " << half << ";\n";
   rsrc_pair(hdr2, "RD", "data", "ds", "stripe", s.k, "");
   rsrc_pair(hdr2, "RO", "out", "os", "stripe", s.m, "");
+  if (dyn) hdr2 << "  const u32 *DM = dm + stripe * dmw;\n";
   if (any_xor) rsrc_pair(hdr2, "RR", "rec", "rs", "stripe", s.m, "");
   hdr2 << "  u32 ";
   for (uint32_t r = 0; r < 8; r++)
@@ -618,11 +627,16 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     if (r0 == r1) return vm;
     o << "  __builtin_amdgcn_sched_barrier(0);\n  {\n";
     if (!full) o << "  const u32 vm = " << mask_expr(vm) << ";\n";
+    if (dyn)  // this wave's 8 positions of chunk j: one byte of the stripe's skip mask
+      o << "  const u32 dsk = (" << (std::string(rd) == "RDn" ? "DMn" : "DM") << "[" << j * C / 32
+        << "u + (w >> 2)] >> ((w & 3u) << 3)) & 0xFFu;\n";
     for (uint32_t r = r0; r < r1; r++) {
       o << "  { const u32 so = (" << j * C + r << "u + (w << 3)) * sbl;\n    ";
       const std::string rd1 = std::string(rd) + "1";
-      const std::string rs = full ? std::string(rd) : "((vm >> " + std::to_string(r) + " & 1u) ? " + rd + " : RZ)";
-      const std::string rs1 = full ? rd1 : "((vm >> " + std::to_string(r) + " & 1u) ? " + rd1 + " : RZ)";
+      std::string cond = full ? "" : "((vm >> " + std::to_string(r) + ") & 1u)";
+      if (dyn) cond = (cond.empty() ? "" : cond + " && ") + "!((dsk >> " + std::to_string(r) + ") & 1u)";
+      const std::string rs = cond.empty() ? std::string(rd) : "(" + cond + " ? " + rd + " : RZ)";
+      const std::string rs1 = cond.empty() ? rd1 : "(" + cond + " ? " + rd1 + " : RZ)";
       o << "la" << j << "[" << r << "] = LDB(" << rs << ", " << uo0 << ", so); lb" << j << "[" << r << "] = LDB(" << rs1
         << ", " << uo1 << ", so); }\n";
     }
@@ -763,6 +777,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   if (pf && xunit) {
     o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = " << (two ? "loff" : "uon + 1024u") << ";\n";
     rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, blocked ? "u + 1u < ue" : "u + gridDim.x < ue");
+    if (dyn) o << "  const u32 *DMn = dm + ((" << (blocked ? "u + 1u < ue" : "u + gridDim.x < ue")
+               << ") ? stripe_n : 0ull) * dmw;\n";
     emit_loads(0, 0, pf, "RDn", "uon", "uon1");
     o << "  }\n";
   }
@@ -809,6 +825,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     }
     // basis change back, planes -> bytes, store (or rec ^ parity)
     g.ops = &g.st->ops_io;
+    if (dyn)  // rows this stripe stores: one byte of its store mask
+      o << "  const u32 dst = (DM[" << dyn_store_word(P) + w / 4 << "u] >> " << (w % 4) * 8 << ") & 0xFFu;\n";
     for (uint32_t r = 0; r < 8; r++) {
       const uint32_t p = P.posA(w, r);
       if (P.out_mode[p] == kOutNone) continue;
@@ -823,7 +841,10 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       g.op(4 + 48);
       o << "    const u32 so = " << p << "u * sbl;\n";
       if (P.out_mode[p] == kOutXorRec) o << "    a ^= LDB(RR, uo, so); b ^= LDB(RR1, uo1, so);\n";
-      o << "    STB(a, RO, uo, so); STB(b, RO1, uo1, so); }\n";
+      if (dyn)
+        o << "    const bool keep = (dst >> " << r << ") & 1u;\n    STB(a, keep ? RO : RZ, uo, so); STB(b, keep ? RO1 : RZ, uo1, so); }\n";
+      else
+        o << "    STB(a, RO, uo, so); STB(b, RO1, uo1, so); }\n";
     }
     g.ops = &g.st->ops_a;
     o << "  }\n";
@@ -860,7 +881,8 @@ std::string cache_key(const Spec &s) {
                   "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + "b" + std::to_string(blocked_of()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
-                  (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "");
+                  (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
+                  (s.dyn ? "dyn:" : "");
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
   k.push_back(':');
   for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));
@@ -877,6 +899,8 @@ std::string kernel_name(const Spec &s) {
 }
 
 std::string generate(const Spec &s, const std::string &name) { return gen_source(s, name, nullptr); }
+
+uint32_t dyn_mask_words(const Spec &s) { return dyn_store_word(make_plan(s)) + 2; }
 
 Stats stats(const Spec &s) {
   Stats st;
@@ -918,10 +942,12 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 }
 
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
-                  uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st) {
+                  uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st, const uint32_t *dmask,
+                  uint32_t dmask_words) {
   if (n_stripes == 0) return hipSuccess;
   if (!supports(s.k, s.m, sb) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
     return hipErrorInvalidValue;
+  if (s.dyn && (s.pieces != 1 || !dmask || dmask_words < dyn_mask_words(s))) return hipErrorInvalidValue;
   const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));
   static std::mutex mu;
   static std::map<int, int> cus;
@@ -947,7 +973,9 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
   uint32_t sb32 = static_cast<uint32_t>(sb);
   const unsigned char *d = data, *r = rec ? rec : data;
   unsigned char *o = out;
-  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st};
+  const uint32_t *dm = dmask;
+  uint32_t dmw = dmask_words;
+  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st, &dm, &dmw};
   return hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(grid), 1, 1, (C / 8) * 64, 1, 1, 0, st, args, nullptr);
 }
 

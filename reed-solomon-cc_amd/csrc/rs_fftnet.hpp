@@ -49,7 +49,13 @@ struct Spec {
   // the encode inverted (k == m == chunk): input = the m recovery shards, IFFT at skew 0,
   // FFT at skew chunk, output = the k originals (reconstruct with every original lost)
   bool inverse = false;
+  // per-stripe masks (launch dmask): the data positions skipped and the rows stored
+  // come from each stripe's mask block instead of skip / out_mode (one stripe per unit)
+  bool dyn = false;
 };
+// u32 words of a stripe's mask block (Spec::dyn): bit p of words [0, w - 2) = data shard
+// p read as zero, bit q of the last 2 words = parity row q stored
+uint32_t dyn_mask_words(const Spec &s);
 
 // the inverse form exists for this code (single full chunk: k == m == chunk)
 bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes);
@@ -76,7 +82,8 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 // data [stripe][k][sb] (stride ds), rec [stripe][m][sb] (rs; read for kOutXorRec rows),
 // out [stripe][m][sb] (os; only the rows out_mode stores are written)
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
-                  uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st);
+                  uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st,
+                  const uint32_t *dmask = nullptr, uint32_t dmask_words = 0);
 
 // Host check of the generator's arithmetic: runs the kernel's schedule with its
 // T-coordinate matrices on scalar symbols and compares with scalar_encode.

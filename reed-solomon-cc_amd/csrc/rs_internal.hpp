@@ -133,6 +133,12 @@ hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uin
                             uint32_t max_e, uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log,
                             uint32_t *plan, uint32_t plan_dw, int32_t *status, hipStream_t s);
 
+// Per-stripe plan of the wide-code path: FFT mask block (dmw words) + solve header
+// (rs_kernels.hip k_wps_plan); plan_dw >= dmw + 2 + 64 + 64 * 8, m <= 64
+hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_e,
+                           uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log, uint32_t *plan,
+                           uint32_t plan_dw, uint32_t dmw, int32_t *status, hipStream_t s);
+
 // present rows trimmed to the k shards the matrix path decodes from (out: [n][k+m])
 hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
                                uint8_t *out, hipStream_t s);

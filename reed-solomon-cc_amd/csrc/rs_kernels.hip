@@ -1259,6 +1259,72 @@ __global__ __launch_bounds__(64) void k_psyn_plan(const uint8_t *__restrict__ pr
   pl[3] = e < max_e ? e : max_e;
 }
 
+// Per-stripe plan of the wide-code path (rs_psyn.hpp solve kernel after the FFT
+// syndrome kernel, chunk 32 / 64): as k_psyn_plan for any e <= m <= 64, one thread per
+// stripe (the e x 2e Gauss-Jordan lives in private memory). Block per stripe (u32):
+// [0, dmw) the FFT kernel's masks (fftnet::dyn_mask_words: erased data bits, then the
+// R rows stored), then at hdr = dmw: [0] outputs stored = min(e, max_e), [1] e,
+// [2, 2 + 64) R, [66 + i * 8 + j] = A^-1[j][i] in polynomial form for j < 8.
+constexpr uint32_t kWpsMaxM = 64, kWpsMaxOut = 8;
+__global__ __launch_bounds__(64) void k_wps_plan(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                 uint32_t k, uint32_t m, uint32_t max_e, uint64_t n,
+                                                 const uint16_t *__restrict__ G, const uint16_t *__restrict__ exp,
+                                                 const uint16_t *__restrict__ log, uint32_t *__restrict__ plan,
+                                                 uint32_t plan_dw, uint32_t dmw, int32_t *__restrict__ status) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint8_t *pr = present + s * present_stride;
+  uint32_t *pl = plan + s * plan_dw, *hd = pl + dmw;
+  uint32_t have = 0, e = 0;
+  for (uint32_t i = 0; i < k + m; i++) have += pr[i] ? 1 : 0;
+  for (uint32_t i = 0; i < k; i++) e += pr[i] ? 0 : 1;
+  if (status) status[s] = have < k ? 2 : (e > max_e ? 14 : 0);  // as k_pattern_tables
+  for (uint32_t i = 0; i < dmw; i++) pl[i] = 0;
+  hd[0] = hd[1] = 0;
+  if (have < k || e == 0) return;
+  uint16_t E[kWpsMaxM], R[kWpsMaxM];
+  for (uint32_t i = 0, c = 0; i < k && c < e; i++)
+    if (!pr[i]) E[c++] = static_cast<uint16_t>(i);
+  for (uint32_t r = 0, c = 0; r < m && c < e; r++)
+    if (pr[k + r]) R[c++] = static_cast<uint16_t>(r);
+  uint16_t A[kWpsMaxM][2 * kWpsMaxM];
+  for (uint32_t i = 0; i < e; i++)
+    for (uint32_t j = 0; j < 2 * e; j++)
+      A[i][j] = static_cast<uint16_t>(j < e ? G[R[i] * k + E[j]] : (j - e == i ? 1u : 0u));
+  for (uint32_t c = 0; c < e; c++) {
+    uint32_t piv = c;
+    while (piv < e && A[piv][c] == 0) piv++;
+    if (piv == e) return;  // singular: cannot happen for an MDS code (nothing restored)
+    for (uint32_t j = 0; j < 2 * e; j++) {
+      const uint16_t t = A[c][j];
+      A[c][j] = A[piv][j];
+      A[piv][j] = t;
+    }
+    const uint32_t inv = exp[(65535u - log[A[c][c]]) % 65535u];
+    for (uint32_t j = c; j < 2 * e; j++) A[c][j] = static_cast<uint16_t>(gf_mul_d(A[c][j], inv, exp, log));
+    for (uint32_t i = 0; i < e; i++)
+      if (i != c && A[i][c]) {
+        const uint32_t f = A[i][c];
+        for (uint32_t j = c; j < 2 * e; j++) A[i][j] ^= static_cast<uint16_t>(gf_mul_d(f, A[c][j], exp, log));
+      }
+  }
+  const uint16_t *cantor = G + m * k;
+  const uint32_t kw = dmw - 2;  // skip words, then 2 store words
+  for (uint32_t i = 0; i < e; i++) {
+    pl[E[i] / 32] |= 1u << (E[i] % 32);
+    pl[kw + R[i] / 32] |= 1u << (R[i] % 32);
+    hd[2 + i] = R[i];
+    for (uint32_t j = 0; j < kWpsMaxOut; j++) {
+      const uint32_t c = j < e ? A[j][e + i] : 0u;
+      uint32_t poly = 0;
+      for (int b = 0; b < 16; b++) poly ^= (c >> b & 1u) ? cantor[b] : 0u;
+      hd[2 + kWpsMaxM + i * kWpsMaxOut + j] = poly;
+    }
+  }
+  hd[1] = e;
+  hd[0] = e < max_e ? e : max_e;
+}
+
 // The matrix path decodes from exactly k received shards (the present originals and
 // the first e present recovery shards), so the erasure locator must be evaluated for
 // that set: present rows with the other recovery shards marked absent.
@@ -1678,6 +1744,18 @@ hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uin
   if (k > 64 || m > kPsynMaxM || max_out > m || plan_dw < 4 + m * max_out) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_psyn_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present, present_stride,
                      k, m, max_out, max_e, n, G, d_exp, d_log, plan, plan_dw, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_e,
+                           uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log, uint32_t *plan,
+                           uint32_t plan_dw, uint32_t dmw, int32_t *status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (m > kWpsMaxM || dmw < 2 || plan_dw < dmw + 2 + kWpsMaxM + kWpsMaxM * kWpsMaxOut ||
+      (dmw - 2) * 32 < k)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_wps_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present, present_stride,
+                     k, m, max_e, n, G, d_exp, d_log, plan, plan_dw, dmw, status);
   return hipGetLastError();
 }
 

@@ -190,6 +190,151 @@ std::string generate(const Spec &s, const std::string &name) {
   return o.str();
 }
 
+namespace {
+// rows of the Cantor <-> polynomial basis changes over bit-planes (rs_gf.hpp cantor_basis):
+// to_poly[c] = mask of Cantor planes feeding polynomial plane c; to_cantor its inverse
+void basis_rows(const uint16_t *cantor, uint16_t *to_poly, uint16_t *to_cantor) {
+  for (int c = 0; c < 16; c++) to_poly[c] = 0;
+  for (int i = 0; i < 16; i++)
+    for (int c = 0; c < 16; c++)
+      if (cantor[i] >> c & 1) to_poly[c] |= static_cast<uint16_t>(1u << i);
+  uint32_t aug[16];
+  for (int c = 0; c < 16; c++) aug[c] = to_poly[c] | (1u << (16 + c));
+  for (int col = 0; col < 16; col++) {
+    int piv = col;
+    while (!(aug[piv] >> col & 1)) piv++;
+    std::swap(aug[piv], aug[col]);
+    for (int r = 0; r < 16; r++)
+      if (r != col && (aug[r] >> col & 1)) aug[r] ^= aug[col];
+  }
+  for (int c = 0; c < 16; c++) to_cantor[c] = static_cast<uint16_t>(aug[c] >> 16);
+}
+
+// x_j ^= c * X for a polynomial-form coefficient held in `cf` (X0..X15 = the input's
+// polynomial planes, consumed): the alpha chain with one uniform branch per set bit
+void emit_chain(std::ostringstream &o, uint32_t j) {
+  std::vector<int> nm(16);
+  for (int c = 0; c < 16; c++) nm[c] = c;
+  for (int i = 0; i < 16; i++) {
+    o << "  if ((cf >> " << i << ") & 1u) {";
+    for (int c = 0; c < 16; c++) o << " x" << j << "_" << c << " ^= X" << nm[c] << ";";
+    o << " }\n";
+    if (i == 15) break;
+    const int top = nm[15];
+    for (int c = 15; c > 0; c--) nm[c] = nm[c - 1];
+    nm[0] = top;
+    o << "  X" << nm[2] << " ^= X" << top << "; X" << nm[3] << " ^= X" << top << "; X" << nm[5] << " ^= X" << top << ";\n";
+  }
+}
+}  // namespace
+
+// The wide-code solve (rs_psyn.hpp launch_solve): one generic kernel, all codes.
+std::string generate_solve(const uint16_t *cantor, const std::string &name) {
+  uint16_t to_poly[16], to_cantor[16];
+  basis_rows(cantor, to_poly, to_cantor);
+  constexpr uint32_t MO = kSolveMaxOut;
+  std::ostringstream o;
+  o << "#define RS_NT 3\n" << jit::net_prelude();
+  o << "extern \"C\" __global__ __launch_bounds__(256) void " << name
+    << "(const unsigned char *__restrict__ rec, u64 rs, const unsigned char *__restrict__ scr, u64 ss,\n"
+       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0, const u32 *__restrict__ plan, u32 pw, u32 hdr) {\n"
+       "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
+       "  const u64 s = stripe0 + blockIdx.y;\n"
+       "  const u64 unit = (u64)blockIdx.x * 4u + (threadIdx.x >> 6);\n"
+       "  if (unit * 4096u >= sb) return;\n"
+       "  const u32 *pl = plan + s * pw + hdr;\n"
+       "  const u32 ne = pl[0], e = pl[1];\n"
+       "  if (ne == 0u) return;\n"
+       "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
+       "  const unsigned char *RB = rec + s * rs, *SB = scr + s * ss;\n"
+       "  unsigned char *O = out + s * so;\n";
+  o << "  u32 ";
+  for (uint32_t j = 0; j < MO; j++)
+    for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << " = 0u" << (j + 1 == MO && c == 15 ? ";\n" : ", ");
+  // syndrome i = rec[R_i] ^ scratch[R_i]; the next one is loaded during this one's work
+  o << "  Raw Rc = ldx(RB + (u64)pl[2] * sb + off, SB + (u64)pl[2] * sb + off);\n"
+       "#pragma unroll 1\n"
+       "  for (u32 i = 0; i < e; i++) {\n"
+       "  Raw Rn = Rc;\n"
+       "  if (i + 1u < e) { const u64 r = pl[3u + i]; Rn = ldx(RB + r * sb + off, SB + r * sb + off); }\n"
+       "  u32 P[16];\n  planes(Rc, P);\n  u32 ";
+  for (int c = 0; c < 16; c++) o << "a" << c << (c == 15 ? ";\n" : ", ");
+  {
+    std::vector<uint16_t> rows(to_poly, to_poly + 16);
+    std::vector<bool> init(16, false);
+    jit::emit_network_input(o, rows, init, 900);
+    for (int c = 0; c < 16; c++)
+      if (!init[c]) o << "  a" << c << " = 0u;\n";
+  }
+  for (uint32_t j = 0; j < MO; j++) {
+    o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << 2 + 64 << "u + i * " << MO << "u + " << j << "u];\n  u32 ";
+    for (int c = 0; c < 16; c++) o << "X" << c << " = a" << c << (c == 15 ? ";\n" : ", ");
+    emit_chain(o, j);
+    o << "  }\n";
+  }
+  o << "  Rc = Rn;\n  }\n";
+  for (uint32_t j = 0; j < MO; j++) {
+    o << "  if (" << j << "u < ne) {\n  u32 P[16] = {";
+    for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << (c == 15 ? "};\n" : ", ");
+    o << "  u32 ";
+    for (int c = 0; c < 16; c++) o << "a" << c << (c == 15 ? ";\n" : ", ");
+    std::vector<uint16_t> rows(to_cantor, to_cantor + 16);
+    std::vector<bool> init(16, false);
+    jit::emit_network_input(o, rows, init, static_cast<int>(1000 + j));
+    for (int c = 0; c < 16; c++)
+      if (!init[c]) o << "  a" << c << " = 0u;\n";
+    o << "  u32 Q[16] = {";
+    for (int c = 0; c < 16; c++) o << "a" << c << (c == 15 ? "};\n" : ", ");
+    o << "  st(O + " << j << "ull * sb + off, Q);\n  }\n";
+  }
+  o << "}\n";
+  return o.str();
+}
+
+const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err) {
+  std::string key = "psolve:o" + std::to_string(kSolveMaxOut) + ":";
+  key.append(reinterpret_cast<const char *>(cantor), 16 * sizeof(uint16_t));
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
+  char name[64];
+  std::snprintf(name, sizeof name, "rs_psyn_solve_o%u_%016llx", kSolveMaxOut, static_cast<unsigned long long>(h));
+  const std::string nm = name;
+  std::vector<uint16_t> cb(cantor, cantor + 16);
+  bool pending = false;
+  return jit::get_source(key, nm, [cb, nm] { return generate_solve(cb.data(), nm); }, false, err, pending);
+}
+
+bool compile_check_solve(const uint16_t *cantor, std::string &err, double *ms, size_t *code_bytes) {
+  const std::string src = generate_solve(cantor, "rs_psyn_solve_check");
+  if (const char *dir = std::getenv("RS_AMD_JIT_DUMP")) {
+    if (FILE *f = std::fopen((std::string(dir) + "/rs_psyn_solve_check.hip").c_str(), "w")) {
+      std::fputs(src.c_str(), f);
+      std::fclose(f);
+    }
+  }
+  return jit::compile_source_check(src, err, ms, code_bytes);
+}
+
+hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_, const uint8_t *scratch, uint64_t ss,
+                        uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
+                        uint32_t plan_dw, uint32_t hdr, hipStream_t st) {
+  if (n_stripes == 0) return hipSuccess;
+  if (sb == 0 || sb % jit::kUnitBytes || sb >= (1ull << 32)) return hipErrorInvalidValue;
+  const uint64_t gx = (sb / jit::kUnitBytes + 3) / 4;
+  for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
+    const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
+    const unsigned char *a0 = rec, *a1 = scratch;
+    unsigned char *o = out;
+    uint64_t st0 = rs_, st1 = ss, so = so_, sbv = sb, first = s0;
+    const uint32_t *pp = plan;
+    uint32_t pw = plan_dw, hd = hdr;
+    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sbv, &first, &pp, &pw, &hd};
+    hipError_t e = hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(gx), gy, 1, 256, 1, 1, 0, st, args, nullptr);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 const jit::Kernel *get(const Spec &s, std::string &err) {
   const std::string name = name_of(s);
   bool pending = false;

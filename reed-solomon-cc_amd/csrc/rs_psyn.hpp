@@ -56,5 +56,19 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *orig, uin
                   uint64_t rs_, uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
                   hipStream_t st);
 
+// Wide codes (chunk 32 / 64, any e <= m <= 64; outputs <= kSolveMaxOut per stripe): the
+// syndromes come from the bit-sliced FFT kernel with per-stripe masks (fftnet::Spec::dyn:
+// erased shards read as zero, only the rows R stored into a scratch), and one generic
+// kernel solves x = A^-1 (rec[R] ^ scratch[R]) with the alpha chains above, a runtime
+// loop over the e syndromes (plan from launch_wps_plan, header at word `hdr` of a
+// stripe's plan_dw-word block).
+constexpr uint32_t kSolveMaxOut = 8;
+std::string generate_solve(const uint16_t *cantor, const std::string &name);
+const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err);
+bool compile_check_solve(const uint16_t *cantor, std::string &err, double *ms, size_t *code_bytes);
+hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_, const uint8_t *scratch, uint64_t ss,
+                        uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
+                        uint32_t plan_dw, uint32_t hdr, hipStream_t st);
+
 }  // namespace psyn
 }  // namespace rs

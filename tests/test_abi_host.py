@@ -209,6 +209,7 @@ def test_psyn_kernel_compiles_for_gfx950():
     outside its range (m > 4, D1 multiply, low rate) have none."""
     assert R.psyn_compile_check(10, 4)["code_bytes"] > 10000
     assert R.psyn_compile_check(4, 2, 2)["code_bytes"] > 1000
+    assert R.psyn_compile_check(100, 20)["code_bytes"] > 10000  # wide: FFT with per-stripe masks + solve
     for k, m, flags in ((5, 5, 0), (10, 4, 1), (2, 4, 0)):
         with pytest.raises(R.InvalidArgument):
             R.psyn_compile_check(k, m, flags)

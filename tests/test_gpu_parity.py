@@ -481,6 +481,39 @@ def test_per_stripe_syndrome_network(oracle, flags, max_e):
         assert (out[s, len(got):] == 0xAB).all(), s
 
 
+@pytest.mark.parametrize("k,m,sb,n", [(200, 55, 8192, 13), (100, 20, 4096, 9), (33, 17, 4096, 7), (64, 64, 4096, 5),
+                                      (40, 50, 8192, 6)])
+@pytest.mark.parametrize("flags", [0, 2])
+def test_per_stripe_wide_codes(oracle, k, m, sb, n, flags):
+    """Wide codes, per-stripe patterns, max_e = 8: syndromes on the FFT kernel with
+    per-stripe masks, then the generic e x e solve (rs_psyn.hpp). Stripes lose 0..12
+    originals (plus some recovery shards); more than 8 restore the first 8 and report 14;
+    too few present report 2 and write nothing."""
+    rng = np.random.default_rng(k * 7 + m + flags)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n - 1):
+        e = int(rng.integers(0, min(12, m) + 1))
+        present[s, rng.choice(k, size=e, replace=False)] = 0
+        present[s, k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
+    present[n - 1, :] = 1
+    present[n - 1, : m + 1] = 0  # not enough shards
+    max_e = 8
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    assert status[n - 1] == 2 and (out[n - 1] == 0xAB).all()
+    for s in range(n - 1):
+        missing = [i for i in range(k) if not present[s, i]]
+        assert status[s] == (14 if len(missing) > max_e else 0), s
+        got = missing[:max_e]
+        assert (out[s, :len(got)] == data[s, got]).all(), (s, missing)
+        assert (out[s, len(got):] == 0xAB).all(), s
+
+
 @pytest.mark.parametrize("sb", [2, 6, 66, 70, 1000, 4102])
 @pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (200, 55)])
 def test_shard_tails_vs_oracle(oracle, k, m, sb):
