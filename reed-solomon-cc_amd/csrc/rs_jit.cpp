@@ -250,7 +250,7 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //                        -1: on above 16 input blocks; off costs nothing to compile
 //                        for small networks and measured ~1.5% faster on RS(10,4))
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1;
 };
 
 int env_int(const char *name, int def) {
@@ -266,12 +266,22 @@ Tuning tuning() {
   t.barrier = env_int("RS_AMD_NET_BARRIER", t.barrier);
   t.units = std::max(1, std::min(64, env_int("RS_AMD_NET_UNITS", t.units)));
   t.tile = env_int("RS_AMD_NET_TILE", t.tile) >= 8 ? 8 : 4;
+  t.shared = env_int("RS_AMD_NET_SHARED", t.shared);
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
   return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt) + "b" +
-         std::to_string(t.barrier) + "u" + std::to_string(t.units) + "t" + std::to_string(t.tile);
+         std::to_string(t.barrier) + "u" + std::to_string(t.units) + "t" + std::to_string(t.tile) + "s" +
+         std::to_string(t.shared);
+}
+
+// Shared-input form (generate_shared): one workgroup of n_tiles waves per 4 KiB unit,
+// the inputs' plane transforms done once and shared through LDS. RS_AMD_NET_SHARED:
+// 1 on, 0 off, -1 (default) off for now — measured per map before enabling.
+bool shared_on(const Tuning &t, const NetSpec &spec) {
+  const uint32_t n_tiles = (spec.n_out + t.tile - 1) / t.tile;
+  return spec.pieces == 1 && n_tiles >= 2 && n_tiles <= 8 && t.shared > 0;
 }
 
 }  // namespace
@@ -308,9 +318,101 @@ std::string generate_with(const NetSpec &spec, const std::string &name, const Tu
 std::string generate(const NetSpec &spec, const std::string &name) { return generate_with(spec, name, tuning()); }
 
 namespace {
+// Shared-input network: a workgroup of T = n_tiles waves covers one 4 KiB unit of a
+// stripe; wave w owns output tile w (its accumulators and its network code). Inputs go
+// in batches of T: wave w loads input bT + w (prefetched one batch ahead), transforms it
+// to planes and writes them to LDS (double-buffered, one barrier per batch), then every
+// wave runs its tile's network over the batch's T inputs read back from LDS. Every input
+// is read from HBM and transposed once instead of once per tile.
+std::string generate_shared(const NetSpec &spec, const std::string &name, const Tuning &tu) {
+  const uint32_t n_in = spec.n_in, n_out = spec.n_out;
+  const uint32_t tw = static_cast<uint32_t>(tu.tile);
+  const uint32_t T = (n_out + tw - 1) / tw, nb = (n_in + T - 1) / T;
+  std::ostringstream o;
+  o << "#define RS_NT " << (std::getenv("RS_AMD_NET_NT") ? tu.nt : 3) << "\n" << kPrelude;
+  o << "extern \"C\" __global__ __launch_bounds__(" << 64 * T << ") ";
+  if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
+  o << "void " << name
+    << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
+       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0,\n"
+       "    const unsigned char *__restrict__ b2, u64 s2, u64 nst) {\n"
+    << "  __shared__ v4 xs[" << 2 * T * 4 * 64 << "];\n"
+       "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
+       "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+       "  const u64 s = stripe0 + blockIdx.y;\n"
+       "  const unsigned char *B0 = b0 + s * s0, *B1 = b1 + s * s1, *B2 = b2 + s * s2;\n"
+       "  unsigned char *O = out + s * so;\n"
+       "  const u32 off = blockIdx.x * 4096u + (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n";
+  auto load_expr = [&](uint32_t t) {
+    const int32_t src = spec.src[t];
+    const uint32_t idx = static_cast<uint32_t>(src & kSrcIndexMask);
+    std::ostringstream e;
+    if (src & kSrcXorScratch)
+      e << "ldx(B1 + " << idx << "ull * sb + off, B2 + " << idx << "ull * sb + off)";
+    else
+      e << "ld(" << ((src & kSrcRecovery) ? "B1" : "B0") << " + " << idx << "ull * sb + off)";
+    return e.str();
+  };
+
+  // one complete path per tile (wave w = tile w): its staging of input bT + w, the
+  // barrier, its network over the batch, for every batch. Disjoint paths keep the
+  // register allocation per tile (one shared path with a branch per batch and tile
+  // merged the tiles' live ranges: 372 VGPRs and spills for RS(32,32)); every path
+  // passes the same number of barriers.
+  for (uint32_t tile = 0; tile < T; tile++) {
+    const uint32_t j0 = tile * tw, nj = std::min(tw, n_out - j0);
+    o << "  " << (tile ? "else if" : "if") << " (w == " << tile << "u) {\n  u32 ";
+    for (size_t r = 0; r < 16 * nj; r++) o << "a" << r << (r + 1 < 16 * nj ? ", " : ";\n");
+    std::vector<bool> init(16 * nj, false);
+    if (tile < n_in) o << "  Raw R = " << load_expr(tile) << ";\n";
+    for (uint32_t bt = 0; bt < nb; bt++) {
+      const uint32_t buf = bt & 1, cnt = std::min(T, n_in - bt * T);
+      o << "  // ---- batch " << bt << ": inputs " << bt * T << ".." << bt * T + cnt - 1 << "\n";
+      if (tile < cnt) {
+        o << "  {\n  u32 P[16];\n  planes(R, P);\n";
+        for (int q = 0; q < 4; q++)
+          o << "  xs[" << (buf * T + tile) * 256 + q * 64 << "u + lane] = (v4){P[" << 4 * q << "], P[" << 4 * q + 1
+            << "], P[" << 4 * q + 2 << "], P[" << 4 * q + 3 << "]};\n";
+        o << "  }\n";
+        if ((bt + 1) * T + tile < n_in) o << "  R = " << load_expr((bt + 1) * T + tile) << ";\n";
+      }
+      o << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\", \"local\");\n"
+           "  __builtin_amdgcn_s_barrier();\n"
+           "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\", \"local\");\n";
+      for (uint32_t i = 0; i < cnt; i++) {
+        const uint32_t t = bt * T + i;
+        o << "  {\n  u32 P[16];\n";
+        for (int q = 0; q < 4; q++)
+          o << "  { const v4 x = xs[" << (buf * T + i) * 256 + q * 64 << "u + lane]; P[" << 4 * q << "] = x[0]; P["
+            << 4 * q + 1 << "] = x[1]; P[" << 4 * q + 2 << "] = x[2]; P[" << 4 * q + 3 << "] = x[3]; }\n";
+        std::vector<uint16_t> rows(16 * nj, 0);
+        for (uint32_t jj = 0; jj < nj; jj++)
+          for (int bb = 0; bb < 16; bb++) {
+            const uint16_t img = spec.images[(static_cast<size_t>(t) * n_out + j0 + jj) * 16 + bb];
+            for (int c = 0; c < 16; c++)
+              if (img >> c & 1) rows[jj * 16 + c] |= static_cast<uint16_t>(1u << bb);
+          }
+        emit_input(o, rows, init, static_cast<int>(t));
+        o << "  }\n  __builtin_amdgcn_sched_barrier(0);\n";
+      }
+    }
+    for (size_t r = 0; r < 16 * nj; r++)
+      if (!init[r]) o << "  a" << r << " = 0u;\n";
+    for (uint32_t jj = 0; jj < nj; jj++) {
+      o << "  { u32 Q[16] = {";
+      for (int c = 0; c < 16; c++) o << "a" << jj * 16 + c << (c < 15 ? ", " : "};\n");
+      o << "    st(O + " << (j0 + jj) << "ull * sb + off, Q); }\n";
+    }
+    o << "  }\n";
+  }
+  o << "}\n";
+  return o.str();
+}
+
 // the knobs are captured when a compile is requested (a background job must not see
 // the environment of a later moment: the cache key already names these values)
 std::string generate_with(const NetSpec &spec, const std::string &name, const Tuning &tu) {
+  if (shared_on(tu, spec)) return generate_shared(spec, name, tu);
   const uint32_t n_in = spec.n_in, n_out = spec.n_out;
   const uint32_t tw = static_cast<uint32_t>(tu.tile);  // outputs per workgroup
   const uint32_t n_tiles = (n_out + tw - 1) / tw;
@@ -618,6 +720,7 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const
   k->n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
   k->units = static_cast<uint32_t>(tu.units);
   k->pieces = spec.pieces;
+  k->shared = shared_on(tu, spec);
   return k;
 }
 
@@ -771,6 +874,7 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
                         k.n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
                         k.units = static_cast<uint32_t>(tu.units);
                         k.pieces = spec.pieces;
+                        k.shared = shared_on(tu, spec);
                       },
                       dev});
   } catch (const std::exception &ex) {  // no worker thread: the table kernel stays in use
@@ -856,6 +960,22 @@ hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const 
                   const uint8_t *buf2, uint64_t stride2) {
   if (n_stripes == 0) return hipSuccess;
   if (k.pieces > 1 && shard_bytes * k.pieces != kUnitBytes) return hipErrorInvalidValue;  // wrong kernel for sb
+  if (k.shared) {  // one workgroup of n_tiles waves per 4 KiB unit (generate_shared)
+    const uint64_t units = shard_bytes / kUnitBytes;
+    if (units == 0 || units > 0x7fffffffull || shard_bytes % kUnitBytes) return hipErrorInvalidValue;
+    for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
+      const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
+      const unsigned char *a0 = buf0, *a1 = buf1 ? buf1 : buf0, *a2 = buf2 ? buf2 : a1;
+      unsigned char *o = out;
+      uint64_t st0 = stride0, st1 = buf1 ? stride1 : stride0, so = out_stride, sb = shard_bytes, first = s0;
+      uint64_t st2 = buf2 ? stride2 : st1, nst = n_stripes;
+      void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sb, &first, &a2, &st2, &nst};
+      hipError_t e = hipModuleLaunchKernel(k.fn, static_cast<uint32_t>(units), gy, 1, 64 * k.n_tiles, 1, 1, 0, s, args,
+                                           nullptr);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   // small shards: one launch row whose wave units each span k.pieces stripes
   const uint64_t units = k.pieces > 1 ? (n_stripes + k.pieces - 1) / k.pieces : shard_bytes / kUnitBytes;
   const uint64_t per_block = 4ull * k.units;

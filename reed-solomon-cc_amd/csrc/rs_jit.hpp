@@ -78,6 +78,7 @@ struct Kernel {
   hipModule_t module = nullptr;
   hipFunction_t fn = nullptr;
   uint32_t n_in = 0, n_out = 0, n_tiles = 0, units = 1, pieces = 1;
+  bool shared = false;  // shared-input form: one workgroup of n_tiles waves per 4 KiB unit
   std::string name;
   double compile_ms = 0;
 };

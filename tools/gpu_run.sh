@@ -5,7 +5,7 @@
 #   bash tools/gpu_run.sh tests -k per_stripe -- sweep --k 32 --m 32 --shard-bytes 1024 \
 #        --stripes 65536 --erase 0 --var RS_AMD_FFT=1,0 -- patterns 2048 -- prof patterns tools/patterns_bench.py 1024
 # steps:
-#   tests [pytest args]       python -m pytest tests -m gpu (600 s)
+#   tests [pytest args]       python -m pytest -m gpu [paths, default tests/] (900 s)
 #   sweep [kernel_sweep args] tools/kernel_sweep.py, JSON lines (300 s)
 #   patterns [args]           tools/patterns_bench.py (300 s)
 #   prof TAG script [args]    rocprofv3 --kernel-trace --stats of a python script (300 s)
@@ -21,7 +21,8 @@ run_step() {
   local log="gpurun_out/step${n}_${kind}.log" rc
   echo "== step $n: $kind $*"
   case $kind in
-    tests) timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 \
+    tests) [ $# -eq 0 ] && set -- tests  # test paths / -k expressions, default the whole suite
+           timeout -k 10 900 python -u -m pytest -m gpu -q -p no:cacheprovider --timeout 300 \
              --timeout-method thread "$@" > "$log" 2>&1 ;;
     sweep) timeout -k 10 300 python -u tools/kernel_sweep.py "$@" > "$log" 2>&1 ;;
     patterns) timeout -k 10 300 python -u tools/patterns_bench.py "$@" > "$log" 2>&1 ;;
