@@ -250,7 +250,7 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //                        -1: on above 16 input blocks; off costs nothing to compile
 //                        for small networks and measured ~1.5% faster on RS(10,4))
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, shared_batch = 1;
 };
 
 int env_int(const char *name, int def) {
@@ -267,21 +267,25 @@ Tuning tuning() {
   t.units = std::max(1, std::min(64, env_int("RS_AMD_NET_UNITS", t.units)));
   t.tile = env_int("RS_AMD_NET_TILE", t.tile) >= 8 ? 8 : 4;
   t.shared = env_int("RS_AMD_NET_SHARED", t.shared);
+  t.shared_batch = env_int("RS_AMD_NET_SHARED_BATCH", t.shared_batch);
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
   return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt) + "b" +
          std::to_string(t.barrier) + "u" + std::to_string(t.units) + "t" + std::to_string(t.tile) + "s" +
-         std::to_string(t.shared);
+         std::to_string(t.shared) + (t.shared_batch != 1 ? "x" + std::to_string(t.shared_batch) : "");
 }
 
 // Shared-input form (generate_shared): one workgroup of n_tiles waves per 4 KiB unit,
 // the inputs' plane transforms done once and shared through LDS. RS_AMD_NET_SHARED:
-// 1 on, 0 off, -1 (default) off for now — measured per map before enabling.
+// 0 off, else (default) on for 2..8 output tiles of whole 4 KiB units. Measured
+// (profiles/r02/sweep_shared_net.jsonl): the RS(200,55) 55 x 55 syndrome map 8.43 ->
+// 6.84 ms reconstruct, RS(16,16) 1 MiB encode 4.16 -> 3.44 ms, RS(64,64) losing 40
+// 3.92 -> 3.26 ms, RS(200,55) losing 20 6.35 -> 5.21 ms.
 bool shared_on(const Tuning &t, const NetSpec &spec) {
   const uint32_t n_tiles = (spec.n_out + t.tile - 1) / t.tile;
-  return spec.pieces == 1 && n_tiles >= 2 && n_tiles <= 8 && t.shared > 0;
+  return spec.pieces == 1 && n_tiles >= 2 && n_tiles <= 8 && t.shared != 0;
 }
 
 }  // namespace
@@ -327,7 +331,11 @@ namespace {
 std::string generate_shared(const NetSpec &spec, const std::string &name, const Tuning &tu) {
   const uint32_t n_in = spec.n_in, n_out = spec.n_out;
   const uint32_t tw = static_cast<uint32_t>(tu.tile);
-  const uint32_t T = (n_out + tw - 1) / tw, nb = (n_in + T - 1) / T;
+  // RS_AMD_NET_SHARED_BATCH: inputs staged per wave between barriers (batch = T * mult)
+  // (two buffers of 4 KiB per staged input within the 160 KiB of LDS)
+  const uint32_t T = (n_out + tw - 1) / tw;
+  const uint32_t mult = std::max(1u, std::min({4u, static_cast<uint32_t>(std::max(1, tu.shared_batch)), 20u / T}));
+  const uint32_t BW = T * mult, nb = (n_in + BW - 1) / BW;
   std::ostringstream o;
   o << "#define RS_NT " << (std::getenv("RS_AMD_NET_NT") ? tu.nt : 3) << "\n" << kPrelude;
   o << "extern \"C\" __global__ __launch_bounds__(" << 64 * T << ") ";
@@ -336,7 +344,7 @@ std::string generate_shared(const NetSpec &spec, const std::string &name, const 
     << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
        "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0,\n"
        "    const unsigned char *__restrict__ b2, u64 s2, u64 nst) {\n"
-    << "  __shared__ v4 xs[" << 2 * T * 4 * 64 << "];\n"
+    << "  __shared__ v4 xs[" << 2 * BW * 4 * 64 << "];\n"
        "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
        "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        "  const u64 s = stripe0 + blockIdx.y;\n"
@@ -364,26 +372,29 @@ std::string generate_shared(const NetSpec &spec, const std::string &name, const 
     o << "  " << (tile ? "else if" : "if") << " (w == " << tile << "u) {\n  u32 ";
     for (size_t r = 0; r < 16 * nj; r++) o << "a" << r << (r + 1 < 16 * nj ? ", " : ";\n");
     std::vector<bool> init(16 * nj, false);
-    if (tile < n_in) o << "  Raw R = " << load_expr(tile) << ";\n";
+    for (uint32_t q = 0; q < mult; q++)  // inputs tile + qT of batch 0
+      if (tile + q * T < n_in) o << "  Raw R" << q << " = " << load_expr(tile + q * T) << ";\n";
     for (uint32_t bt = 0; bt < nb; bt++) {
-      const uint32_t buf = bt & 1, cnt = std::min(T, n_in - bt * T);
-      o << "  // ---- batch " << bt << ": inputs " << bt * T << ".." << bt * T + cnt - 1 << "\n";
-      if (tile < cnt) {
-        o << "  {\n  u32 P[16];\n  planes(R, P);\n";
-        for (int q = 0; q < 4; q++)
-          o << "  xs[" << (buf * T + tile) * 256 + q * 64 << "u + lane] = (v4){P[" << 4 * q << "], P[" << 4 * q + 1
-            << "], P[" << 4 * q + 2 << "], P[" << 4 * q + 3 << "]};\n";
+      const uint32_t buf = bt & 1, cnt = std::min(BW, n_in - bt * BW);
+      o << "  // ---- batch " << bt << ": inputs " << bt * BW << ".." << bt * BW + cnt - 1 << "\n";
+      for (uint32_t q = 0; q < mult; q++) {
+        const uint32_t slot = tile + q * T;
+        if (slot >= cnt) continue;
+        o << "  {\n  u32 P[16];\n  planes(R" << q << ", P);\n";
+        for (int qq = 0; qq < 4; qq++)
+          o << "  xs[" << (buf * BW + slot) * 256 + qq * 64 << "u + lane] = (v4){P[" << 4 * qq << "], P[" << 4 * qq + 1
+            << "], P[" << 4 * qq + 2 << "], P[" << 4 * qq + 3 << "]};\n";
         o << "  }\n";
-        if ((bt + 1) * T + tile < n_in) o << "  R = " << load_expr((bt + 1) * T + tile) << ";\n";
+        if ((bt + 1) * BW + slot < n_in) o << "  R" << q << " = " << load_expr((bt + 1) * BW + slot) << ";\n";
       }
       o << "  __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"workgroup\", \"local\");\n"
            "  __builtin_amdgcn_s_barrier();\n"
            "  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"workgroup\", \"local\");\n";
       for (uint32_t i = 0; i < cnt; i++) {
-        const uint32_t t = bt * T + i;
+        const uint32_t t = bt * BW + i;
         o << "  {\n  u32 P[16];\n";
         for (int q = 0; q < 4; q++)
-          o << "  { const v4 x = xs[" << (buf * T + i) * 256 + q * 64 << "u + lane]; P[" << 4 * q << "] = x[0]; P["
+          o << "  { const v4 x = xs[" << (buf * BW + i) * 256 + q * 64 << "u + lane]; P[" << 4 * q << "] = x[0]; P["
             << 4 * q + 1 << "] = x[1]; P[" << 4 * q + 2 << "] = x[2]; P[" << 4 * q + 3 << "] = x[3]; }\n";
         std::vector<uint16_t> rows(16 * nj, 0);
         for (uint32_t jj = 0; jj < nj; jj++)
