@@ -857,9 +857,12 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
 }  // namespace
 
 bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
-  if (!basis().ok || m < 17 || m > 64 || k == 0) return false;
+  // chunk 16 (9 <= m <= 16, two waves per workgroup): RS_AMD_FFT_C16=0 keeps those codes
+  // on the networks
+  const uint64_t m_min = env_int("RS_AMD_FFT_C16", 0) ? 9 : 17;
+  if (!basis().ok || m < m_min || m > 64 || k == 0) return false;
   const uint64_t C = ceil_pow2(m);
-  if (C != 32 && C != 64) return false;
+  if (C != 16 && C != 32 && C != 64) return false;
   // high rate (root.zig:397-415) with this chunk
   const uint64_t pk = ceil_pow2(k);
   if (!(pk > C || (pk == C && k <= m))) return false;
@@ -968,7 +971,7 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
   uint64_t n_units = s.pieces > 1 ? (n_stripes + 1) / 2 : n_stripes * ups;
   uint64_t n_st = n_stripes;
   // one workgroup per CU (128 KiB of LDS for chunk 64), persistent over the units
-  const uint32_t per_cu = C == 64 ? 1 : 2;
+  const uint32_t per_cu = C == 64 ? 1 : C == 32 ? 2 : 4;  // LDS 128 / 64 / 32 KiB per workgroup
   const uint64_t grid = std::min<uint64_t>(n_units, static_cast<uint64_t>(n_cu) * per_cu);
   uint32_t sb32 = static_cast<uint32_t>(sb);
   const unsigned char *d = data, *r = rec ? rec : data;

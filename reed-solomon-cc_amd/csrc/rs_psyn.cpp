@@ -24,10 +24,12 @@ int env_int(const char *name, int def) {
 }
 // code-shape knobs (part of the cache key): inputs loaded ahead, occupancy hint
 uint32_t prefetch() { return static_cast<uint32_t>(std::max(0, std::min(6, env_int("RS_AMD_PSYN_PF", 2)))); }
-int waves() { return std::max(0, std::min(8, env_int("RS_AMD_PSYN_WAVES", 3))); }  // 3: 5.19 -> 5.07 ms (profiles/r02/patterns_psyn.jsonl)
+int waves() { return std::max(0, std::min(8, env_int("RS_AMD_PSYN_WAVES", 3))); }
+bool skip_erased() { return env_int("RS_AMD_PSYN_SKIP", 1) != 0; }  // 3: 5.19 -> 5.07 ms (profiles/r02/patterns_psyn.jsonl)
 
 std::string key_of(const Spec &s) {
-  std::string k = "psyn:p" + std::to_string(prefetch()) + "w" + std::to_string(waves()) + ":" + std::to_string(s.k) +
+  std::string k = "psyn:p" + std::to_string(prefetch()) + "w" + std::to_string(waves()) + "s" +
+                  std::to_string(skip_erased()) + ":" + std::to_string(s.k) +
                   ":" + std::to_string(s.m) + ":" + std::to_string(s.flags) + ":";
   k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
   k.append(reinterpret_cast<const char *>(s.cantor.data()), s.cantor.size() * sizeof(uint16_t));
@@ -107,6 +109,12 @@ std::string generate(const Spec &s, const std::string &name) {
   for (uint32_t i = 0; i < PF; i++) load(i);
   for (uint32_t i = 0; i < n_inputs; i++) {
     load(i + PF);
+    // RS_AMD_PSYN_SKIP: an erased input (read as zeros) skips its transform and network
+    // under a wave-uniform branch; its load stays unconditional (prefetch order)
+    if (skip_erased())
+      o << "  if (!(" << (i < K ? std::string(i < 32 ? "(em0 >> " : "(em1 >> ") + std::to_string(i % 32) + ") & 1u"
+                                : "!((rm >> " + std::to_string(i - K) + ") & 1u)")
+        << "))";
     o << "  {\n  u32 P[16];\n  planes(R" << i << ", P);\n";
     std::vector<uint16_t> rows(n_acc, 0);
     if (i < K) {

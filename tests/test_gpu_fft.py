@@ -15,7 +15,9 @@ from rs_amd import reedsol_amd as R  # noqa: E402
 DEV = torch.device("cuda:0")
 
 SHAPES = [(200, 55), (100, 20), (64, 64), (32, 32), (40, 50), (300, 40), (128, 33), (33, 17), (256, 64),
-          (1000, 64), (65, 64)]
+          (1000, 64), (65, 64),
+          # chunk 16 (two waves per workgroup)
+          (16, 16), (40, 12), (100, 16), (9, 9), (20, 9), (17, 16), (64, 10)]
 
 
 def enc(k, m, data, flags=0):
