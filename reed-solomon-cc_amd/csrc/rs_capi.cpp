@@ -142,6 +142,20 @@ uint32_t async_after() {
 // faster there (RS(10,4) 2 KiB 0.644 vs 0.678 ms, RS(4,2) 1 KiB 0.528 vs 0.541 ms,
 // profiles/r01/sweep_small_shard_networks.jsonl); reconstructs take the networks
 // (RS(10,4) 1 KiB losing 4: 1.16 -> 0.67 ms). RS_AMD_NET_SMALL_ENCODE=1 overrides.
+// Encode maps past the synchronous network cap run as background-compiled networks when
+// they take the shared-input form (2..8 output tiles) and no FFT kernel covers the code:
+// RS(40,12) 1 MiB encode 4.10 -> 2.96 ms, RS(100,16) 256 KiB 2.23 -> 1.90 ms against the
+// table register kernel (profiles/r02/sweep_encode_async_net.jsonl); a single tile past
+// the cap keeps the table kernels (round 1: RS(100,20) register kernel 2.97 vs 3.35 ms).
+bool encode_net_async(uint64_t k, uint64_t m) {
+  const char *e = std::getenv("RS_AMD_NET_ASYNC_ENCODE");
+  if (e && *e && std::strcmp(e, "0") == 0) return false;
+  const char *sh = std::getenv("RS_AMD_NET_SHARED");
+  if (sh && *sh && std::strcmp(sh, "0") == 0) return false;
+  return m > 8 && m <= jit::kMaxOut && !fftnet::supports(k, m, fftnet::kUnitBytes) &&
+         jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes);
+}
+
 bool encode_net_ok(uint64_t sb) {
   if (jit::net_pieces(sb) == 1) return true;
   const char *e = std::getenv("RS_AMD_NET_SMALL_ENCODE");
@@ -367,9 +381,9 @@ void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *pres
 // root.zig:136-173 chunk schedule -> table block
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out) {
   char key[128];
-  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu/%llu", dev, (unsigned long long)k, (unsigned long long)m,
+  std::snprintf(key, sizeof key, "%d/%llu/%llu/%u/%llu/%llu/%d", dev, (unsigned long long)k, (unsigned long long)m,
                 flags, static_cast<unsigned long long>(jit::max_blocks()),
-                static_cast<unsigned long long>(jit::max_async_blocks()));
+                static_cast<unsigned long long>(jit::max_async_blocks()), encode_net_async(k, m) ? 1 : 0);
   {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     if ((out = g_enc_plans.find(key))) return RS_OK;
@@ -391,6 +405,9 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   plan->work = static_cast<uint32_t>((k + C - 1) / C * C);
   if (jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes)) {
     encode_map(k, m, flags, plan->net->spec);
+  } else if (encode_net_async(k, m)) {
+    encode_map(k, m, flags, plan->net->spec);
+    plan->net->async = true;
   }
   if (fftnet::supports(k, m, fftnet::kUnitBytes)) {
     plan->fft = std::make_shared<FftSlot>();
@@ -1082,7 +1099,10 @@ const char *rs_encode_kernel_name(uint64_t k, uint64_t m, size_t sb) {
     return "lowrate_matrix";
   }
   if (fft_enabled() && fftnet::supports(k, m, sb)) return net_name("fft_encode", k, m);
-  if (jit::enabled() && encode_net_ok(sb) && jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))
+  if (jit::enabled() && encode_net_ok(sb) &&
+      (jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb) ||
+       (encode_net_async(k, m) && jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb) &&
+        jit::net_pieces(sb) == 1)))
     return net_name("encode", k, m);
   return choose_encode(k, m, sb, 4).name;
 }
@@ -1302,7 +1322,9 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
       }
     }
     if (max_nv == 4 && jit::enabled() && plan->net->spec.n_in && encode_net_ok(sb) &&
-        jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb)) {
+        (plan->net->async ? jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb) &&
+                                jit::net_pieces(sb) == 1
+                          : jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb))) {
       if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride, nullptr, 0,
                             static_cast<uint8_t *>(d_recovery), rec_stride, sb, n_stripes, s));

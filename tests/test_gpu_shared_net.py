@@ -54,3 +54,28 @@ def test_shared_reconstruct(oracle, shared, k, m, lost):
     R.reconstruct_batch_dev(k, m, present, d, torch.from_numpy(par).to(DEV), out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), data[:, lost]), R.reconstruct_kernel_name(k, m, sb, present)
+
+
+@pytest.mark.parametrize("k,m", [(40, 12), (200, 10)])
+def test_encode_background_shared_network(oracle, monkeypatch, k, m):
+    """Encode maps past the synchronous cap (m > 8, no FFT form): table kernels until the
+    background compile of the shared-input network lands, the network after; all equal
+    the oracle."""
+    monkeypatch.delenv("RS_AMD_JIT_SYNC", raising=False)
+    sb, n = 8192, 2
+    assert R.encode_kernel_name(k, m, sb) == f"net_encode_i{k}_o{m}"
+    rng = np.random.default_rng(k * 3 + m)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    exp = oracle.encode_batch(k, m, data)
+    d = torch.from_numpy(data).to(DEV)
+
+    def enc():
+        p = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+        R.encode_batch_dev(k, m, d, p)
+        torch.cuda.synchronize()
+        return p.cpu().numpy()
+
+    for _ in range(3):
+        assert np.array_equal(enc(), exp)
+    R.net_wait()
+    assert np.array_equal(enc(), exp)
