@@ -142,17 +142,19 @@ uint32_t async_after() {
 // faster there (RS(10,4) 2 KiB 0.644 vs 0.678 ms, RS(4,2) 1 KiB 0.528 vs 0.541 ms,
 // profiles/r01/sweep_small_shard_networks.jsonl); reconstructs take the networks
 // (RS(10,4) 1 KiB losing 4: 1.16 -> 0.67 ms). RS_AMD_NET_SMALL_ENCODE=1 overrides.
-// Encode maps past the synchronous network cap run as background-compiled networks when
-// they take the shared-input form (2..8 output tiles) and no FFT kernel covers the code:
-// RS(40,12) 1 MiB encode 4.10 -> 2.96 ms, RS(100,16) 256 KiB 2.23 -> 1.90 ms against the
-// table register kernel (profiles/r02/sweep_encode_async_net.jsonl); a single tile past
-// the cap keeps the table kernels (round 1: RS(100,20) register kernel 2.97 vs 3.35 ms).
+// Encode maps past the synchronous network cap that no FFT kernel covers run as
+// background-compiled networks (table kernels until they land): with the shared-input
+// form for several tiles and one tile otherwise, every shape measured is faster than the
+// table register kernel — RS(40,12) 1 MiB 4.08 -> 2.95 ms, RS(100,6) 2.85 -> 2.35 ms,
+// RS(100,4) 2.49 -> 2.30 ms, RS(200,8) 2.75 -> 2.58 ms (profiles/r02/sweep_encode_async_net.jsonl).
 bool encode_net_async(uint64_t k, uint64_t m) {
   const char *e = std::getenv("RS_AMD_NET_ASYNC_ENCODE");
   if (e && *e && std::strcmp(e, "0") == 0) return false;
   const char *sh = std::getenv("RS_AMD_NET_SHARED");
   if (sh && *sh && std::strcmp(sh, "0") == 0) return false;
-  return m > 8 && m <= jit::kMaxOut && !fftnet::supports(k, m, fftnet::kUnitBytes) &&
+  const char *lo = std::getenv("RS_AMD_NET_ASYNC_ENCODE_MIN_M");
+  const uint64_t m_min = lo && *lo ? static_cast<uint64_t>(std::atoi(lo)) : 1;
+  return m >= m_min && m <= jit::kMaxOut && !fftnet::supports(k, m, fftnet::kUnitBytes) &&
          jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes);
 }
 
