@@ -495,7 +495,15 @@ uint64_t fft_encode_mul_count(uint64_t k, uint64_t m) {
 }
 
 // a direct n_in -> e reconstruct map past the synchronous cap, within the background one
-bool direct_net_async(uint64_t e, uint64_t n_in, uint64_t sb, const std::string &mode) {
+// A direct map past the synchronous cap, compiled in the background. For codes with an
+// FFT kernel a large map loses to the syndrome path (FFT encode + e x e map): RS(200,55)
+// losing 20 5.21 vs 3.90 ms, losing 14 3.56 vs 3.54, losing 8 2.61 vs 3.26 ms
+// (profiles/r02/sweep_direct_vs_syndrome.jsonl), hence the n_in * e bound.
+bool syndrome_pick(uint64_t k, uint64_t m, uint64_t e, uint32_t flags, uint64_t sb, const std::string &mode);
+bool direct_net_async(uint64_t e, uint64_t n_in, uint64_t sb, const std::string &mode, uint64_t k, uint64_t m) {
+  if (mode == "auto" && fft_enabled() && fftnet::supports(k, m, sb) && n_in * e >= 2800 &&
+      syndrome_pick(k, m, e, 0, sb, mode))
+    return false;
   return (mode == "auto" || mode == "net") && jit::enabled() &&
          !jit::supports(static_cast<uint32_t>(n_in), static_cast<uint32_t>(e), sb) &&
          jit::supports_async(static_cast<uint32_t>(n_in), static_cast<uint32_t>(e), sb);
@@ -600,7 +608,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
   // past the synchronous cap: the same map compiled in the background, the matrix
   // kernel meanwhile (RS(200,55) losing 8: 400 blocks, against syndrome + encode)
-  const bool use_net_async = !use_net && kind != 0 && direct_net_async(e, n_in_want, sb, mode);
+  const bool use_net_async = !use_net && kind != 0 && direct_net_async(e, n_in_want, sb, mode, k, m);
   const bool use_syn = !use_net && !use_net_async && syndrome_pick(k, m, e, flags, sb, mode);
   if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
   // the syndromes' e x e map as a network too (its table kernel stays the fallback)
@@ -1128,7 +1136,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
     return net_name("reconstruct", k, e);
-  if (decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode))
+  if (decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode, k, m))
     return net_name("reconstruct", k, e);
   if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
     thread_local std::string name;
