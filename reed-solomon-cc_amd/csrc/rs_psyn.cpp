@@ -46,6 +46,44 @@ std::string name_of(const Spec &s) {
 
 }  // namespace
 
+namespace {
+// rows of the Cantor <-> polynomial basis changes over bit-planes (rs_gf.hpp cantor_basis):
+// to_poly[c] = mask of Cantor planes feeding polynomial plane c; to_cantor its inverse
+void basis_rows(const uint16_t *cantor, uint16_t *to_poly, uint16_t *to_cantor) {
+  for (int c = 0; c < 16; c++) to_poly[c] = 0;
+  for (int i = 0; i < 16; i++)
+    for (int c = 0; c < 16; c++)
+      if (cantor[i] >> c & 1) to_poly[c] |= static_cast<uint16_t>(1u << i);
+  uint32_t aug[16];
+  for (int c = 0; c < 16; c++) aug[c] = to_poly[c] | (1u << (16 + c));
+  for (int col = 0; col < 16; col++) {
+    int piv = col;
+    while (!(aug[piv] >> col & 1)) piv++;
+    std::swap(aug[piv], aug[col]);
+    for (int r = 0; r < 16; r++)
+      if (r != col && (aug[r] >> col & 1)) aug[r] ^= aug[col];
+  }
+  for (int c = 0; c < 16; c++) to_cantor[c] = static_cast<uint16_t>(aug[c] >> 16);
+}
+
+// x_j ^= c * X for a polynomial-form coefficient held in `cf` (X0..X15 = the input's
+// polynomial planes, consumed): the alpha chain with one uniform branch per set bit
+void emit_chain(std::ostringstream &o, uint32_t j) {
+  std::vector<int> nm(16);
+  for (int c = 0; c < 16; c++) nm[c] = c;
+  for (int i = 0; i < 16; i++) {
+    o << "  if ((cf >> " << i << ") & 1u) {";
+    for (int c = 0; c < 16; c++) o << " x" << j << "_" << c << " ^= X" << nm[c] << ";";
+    o << " }\n";
+    if (i == 15) break;
+    const int top = nm[15];
+    for (int c = 15; c > 0; c--) nm[c] = nm[c - 1];
+    nm[0] = top;
+    o << "  X" << nm[2] << " ^= X" << top << "; X" << nm[3] << " ^= X" << top << "; X" << nm[5] << " ^= X" << top << ";\n";
+  }
+}
+}  // namespace
+
 std::string generate(const Spec &s, const std::string &name) {
   const uint32_t K = s.k, M = s.m, MO = max_out(s.k, s.m), PDW = plan_dwords(s.k, s.m);
   std::ostringstream o;
@@ -78,10 +116,8 @@ std::string generate(const Spec &s, const std::string &name) {
   // syndromes s_r = p_r ^ Enc_r(data with E read as zero): the code's fixed network,
   // its rows composed with the Cantor -> polynomial basis change (poly bit c of a
   // symbol = XOR of its Cantor bits i with bit c of cantor[i])
-  uint16_t to_poly[16] = {};  // to_poly[c]: mask of Cantor planes feeding polynomial plane c
-  for (int i = 0; i < 16; i++)
-    for (int c = 0; c < 16; c++)
-      if (s.cantor[i] >> c & 1) to_poly[c] |= static_cast<uint16_t>(1u << i);
+  uint16_t to_poly[16], to_cantor[16];
+  basis_rows(s.cantor.data(), to_poly, to_cantor);
   auto compose = [&](const std::vector<uint16_t> &rows) {  // rows over Cantor output planes -> poly
     std::vector<uint16_t> out(rows.size(), 0);
     for (size_t r = 0; r < rows.size() / 16; r++)
@@ -146,40 +182,13 @@ std::string generate(const Spec &s, const std::string &name) {
       // correlated conditions let the compiler thread and duplicate blocks)
       o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << 4 + r * MO + j << "];\n  u32 ";
       for (int c = 0; c < 16; c++) o << "X" << c << " = a" << r * 16 + c << (c == 15 ? ";\n" : ", ");
-      std::vector<int> nm(16);  // nm[c]: variable X<nm[c]> holds polynomial plane c
-      for (int c = 0; c < 16; c++) nm[c] = c;
-      for (int i = 0; i < 16; i++) {
-        o << "  if ((cf >> " << i << ") & 1u) {";
-        for (int c = 0; c < 16; c++) o << " x" << j << "_" << c << " ^= X" << nm[c] << ";";
-        o << " }\n";
-        if (i == 15) break;
-        const int top = nm[15];  // times alpha: planes move up one, the top folds into 0, 2, 3, 5
-        for (int c = 15; c > 0; c--) nm[c] = nm[c - 1];
-        nm[0] = top;
-        o << "  X" << nm[2] << " ^= X" << top << "; X" << nm[3] << " ^= X" << top << "; X" << nm[5] << " ^= X" << top
-          << ";\n";
-      }
+      emit_chain(o, j);
       o << "  }\n";
     }
     o << "  }\n  __builtin_amdgcn_sched_barrier(0);\n";
   }
   // back to Cantor coordinates (Cantor bit c = XOR of polynomial bits b with bit c of
   // the inverse basis change's column b), then store
-  uint16_t to_cantor[16] = {};  // to_cantor[c]: mask of polynomial planes feeding Cantor plane c
-  {
-    uint32_t M2[16];  // invert to_poly over GF(2): rows of [to_poly | I]
-    uint32_t aug[16];
-    for (int c = 0; c < 16; c++) aug[c] = to_poly[c] | (1u << (16 + c));
-    for (int col = 0; col < 16; col++) {
-      int piv = col;
-      while (!(aug[piv] >> col & 1)) piv++;
-      std::swap(aug[piv], aug[col]);
-      for (int r = 0; r < 16; r++)
-        if (r != col && (aug[r] >> col & 1)) aug[r] ^= aug[col];
-    }
-    for (int c = 0; c < 16; c++) M2[c] = aug[c] >> 16;
-    for (int c = 0; c < 16; c++) to_cantor[c] = static_cast<uint16_t>(M2[c]);
-  }
   for (uint32_t j = 0; j < MO; j++) {
     o << "  if (" << j << "u < ne) {\n  u32 P[16] = {";
     for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << (c == 15 ? "};\n" : ", ");
@@ -198,43 +207,6 @@ std::string generate(const Spec &s, const std::string &name) {
   return o.str();
 }
 
-namespace {
-// rows of the Cantor <-> polynomial basis changes over bit-planes (rs_gf.hpp cantor_basis):
-// to_poly[c] = mask of Cantor planes feeding polynomial plane c; to_cantor its inverse
-void basis_rows(const uint16_t *cantor, uint16_t *to_poly, uint16_t *to_cantor) {
-  for (int c = 0; c < 16; c++) to_poly[c] = 0;
-  for (int i = 0; i < 16; i++)
-    for (int c = 0; c < 16; c++)
-      if (cantor[i] >> c & 1) to_poly[c] |= static_cast<uint16_t>(1u << i);
-  uint32_t aug[16];
-  for (int c = 0; c < 16; c++) aug[c] = to_poly[c] | (1u << (16 + c));
-  for (int col = 0; col < 16; col++) {
-    int piv = col;
-    while (!(aug[piv] >> col & 1)) piv++;
-    std::swap(aug[piv], aug[col]);
-    for (int r = 0; r < 16; r++)
-      if (r != col && (aug[r] >> col & 1)) aug[r] ^= aug[col];
-  }
-  for (int c = 0; c < 16; c++) to_cantor[c] = static_cast<uint16_t>(aug[c] >> 16);
-}
-
-// x_j ^= c * X for a polynomial-form coefficient held in `cf` (X0..X15 = the input's
-// polynomial planes, consumed): the alpha chain with one uniform branch per set bit
-void emit_chain(std::ostringstream &o, uint32_t j) {
-  std::vector<int> nm(16);
-  for (int c = 0; c < 16; c++) nm[c] = c;
-  for (int i = 0; i < 16; i++) {
-    o << "  if ((cf >> " << i << ") & 1u) {";
-    for (int c = 0; c < 16; c++) o << " x" << j << "_" << c << " ^= X" << nm[c] << ";";
-    o << " }\n";
-    if (i == 15) break;
-    const int top = nm[15];
-    for (int c = 15; c > 0; c--) nm[c] = nm[c - 1];
-    nm[0] = top;
-    o << "  X" << nm[2] << " ^= X" << top << "; X" << nm[3] << " ^= X" << top << "; X" << nm[5] << " ^= X" << top << ";\n";
-  }
-}
-}  // namespace
 
 // The wide-code solve (rs_psyn.hpp launch_solve): one generic kernel, all codes.
 std::string generate_solve(const uint16_t *cantor, const std::string &name) {
