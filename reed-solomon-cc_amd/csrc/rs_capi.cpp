@@ -2198,6 +2198,80 @@ struct DevMem {
     if (p) (void)hipFree(p);
   }
 };
+
+// One-shot calls (rs_encode / rs_decode and the Encoder / Decoder objects, root.zig:14-84)
+// move one stripe: a pooled context per call in flight holds a pinned host buffer, a
+// device buffer and a stream, so a call packs its shards into pinned memory and makes
+// one H2D copy, the kernel and one D2H copy with a single synchronisation (instead of
+// two hipMallocs and k + m synchronous copies). Contexts are kept for reuse (never freed:
+// process-lifetime, like the plan caches' device tables).
+struct OneShot {
+  int dev = -1;
+  hipStream_t s = nullptr;
+  uint8_t *h = nullptr, *d = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_oneshot_mu;
+std::vector<OneShot *> g_oneshot_free;
+
+int oneshot_acquire(int dev, size_t bytes, OneShot **out) {
+  OneShot *c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_oneshot_mu);
+    for (size_t i = 0; i < g_oneshot_free.size(); i++)
+      if (g_oneshot_free[i]->dev == dev) {
+        c = g_oneshot_free[i];
+        g_oneshot_free.erase(g_oneshot_free.begin() + static_cast<std::ptrdiff_t>(i));
+        break;
+      }
+  }
+  if (!c) {
+    c = new OneShot;
+    c->dev = dev;
+    hipError_t e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return hip_fail(e, "hipStreamCreateWithFlags");
+    }
+  }
+  if (c->bytes < bytes) {  // grow to the next power of two
+    size_t nb = 1 << 16;
+    while (nb < bytes) nb <<= 1;
+    if (c->h) (void)hipHostFree(c->h);
+    if (c->d) (void)hipFree(c->d);
+    c->h = c->d = nullptr;
+    c->bytes = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c->h), nb, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->d), nb);
+    if (e != hipSuccess) {
+      if (c->h) (void)hipHostFree(c->h);
+      c->h = nullptr;
+      std::lock_guard<std::mutex> lk(g_oneshot_mu);
+      g_oneshot_free.push_back(c);
+      return hip_fail(e, "one-shot staging buffers");
+    }
+    c->bytes = nb;
+  }
+  *out = c;
+  return RS_OK;
+}
+
+void oneshot_release(OneShot *c) {
+  std::lock_guard<std::mutex> lk(g_oneshot_mu);
+  g_oneshot_free.push_back(c);
+}
+
+struct OneShotLease {  // drains the stream and returns the context on every exit path
+  OneShot *c = nullptr;
+  ~OneShotLease() {
+    if (c) {
+      (void)hipStreamSynchronize(c->s);
+      oneshot_release(c);
+    }
+  }
+};
+
+inline size_t align256(size_t x) { return (x + 255) & ~static_cast<size_t>(255); }
 }  // namespace
 
 int rs_encode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, uint8_t *const *recovery_out) {
@@ -2210,14 +2284,17 @@ int rs_encode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original,
     if (!recovery_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL recovery_out");
     int dev;
     if ((st = current_device(&dev))) return st;
-    DevMem din, dout;
-    HIP_TRY(hipMalloc(&din.p, k * sb));
-    HIP_TRY(hipMalloc(&dout.p, m * sb));
-    for (uint64_t i = 0; i < k; i++)
-      HIP_TRY(hipMemcpy(static_cast<uint8_t *>(din.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
-    if ((st = rs_encode_batch_dev(k, m, sb, 1, din.p, 0, dout.p, 0, RS_FLAG_CORRECTED, nullptr))) return st;
-    for (uint64_t r = 0; r < m; r++)
-      HIP_TRY(hipMemcpy(recovery_out[r], static_cast<uint8_t *>(dout.p) + r * sb, sb, hipMemcpyDeviceToHost));
+    const size_t off = align256(k * sb);
+    OneShotLease lease;
+    if ((st = oneshot_acquire(dev, off + m * sb, &lease.c))) return st;
+    OneShot &c = *lease.c;
+    for (uint64_t i = 0; i < k; i++) std::memcpy(c.h + i * sb, original[i], sb);
+    HIP_TRY(hipMemcpyAsync(c.d, c.h, k * sb, hipMemcpyHostToDevice, c.s));
+    st = rs_encode_batch_dev(k, m, sb, 1, c.d, 0, c.d + off, 0, RS_FLAG_CORRECTED, c.s);
+    if (st == RS_OK) HIP_TRY(hipMemcpyAsync(c.h + off, c.d + off, m * sb, hipMemcpyDeviceToHost, c.s));
+    HIP_TRY(hipStreamSynchronize(c.s));  // also drains a failed call's queued copy
+    if (st) return st;
+    for (uint64_t r = 0; r < m; r++) std::memcpy(recovery_out[r], c.h + off + r * sb, sb);
     return RS_OK;
   });
 }
@@ -2244,24 +2321,25 @@ int rs_decode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original,
     if (e > 0) {
       int dev;
       if ((st = current_device(&dev))) return st;
-      DevMem dorig, drec, dout;
-      HIP_TRY(hipMalloc(&dorig.p, k * sb));
-      HIP_TRY(hipMalloc(&drec.p, m * sb));
-      HIP_TRY(hipMalloc(&dout.p, e * sb));
+      // staging: [originals k][recovery m][restored e], each region 256-B aligned; absent
+      // slots are not filled (the kernels never read them)
+      const size_t o_rec = align256(k * sb), o_out = o_rec + align256(m * sb);
+      OneShotLease lease;
+      if ((st = oneshot_acquire(dev, o_out + e * sb, &lease.c))) return st;
+      OneShot &c = *lease.c;
       for (uint64_t i = 0; i < k; i++)
-        if (original[i])
-          HIP_TRY(hipMemcpy(static_cast<uint8_t *>(dorig.p) + i * sb, original[i], sb, hipMemcpyHostToDevice));
+        if (original[i]) std::memcpy(c.h + i * sb, original[i], sb);
       for (uint64_t i = 0; i < m; i++)
-        if (recovery[i])
-          HIP_TRY(hipMemcpy(static_cast<uint8_t *>(drec.p) + i * sb, recovery[i], sb, hipMemcpyHostToDevice));
-      if ((st = rs_reconstruct_batch_dev(k, m, sb, 1, present.data(), dorig.p, 0, drec.p, 0, dout.p, 0,
-                                         RS_FLAG_CORRECTED, nullptr)))
-        return st;
+        if (recovery[i]) std::memcpy(c.h + o_rec + i * sb, recovery[i], sb);
+      HIP_TRY(hipMemcpyAsync(c.d, c.h, o_rec + m * sb, hipMemcpyHostToDevice, c.s));
+      st = rs_reconstruct_batch_dev(k, m, sb, 1, present.data(), c.d, 0, c.d + o_rec, 0, c.d + o_out, 0,
+                                    RS_FLAG_CORRECTED, c.s);
+      if (st == RS_OK) HIP_TRY(hipMemcpyAsync(c.h + o_out, c.d + o_out, e * sb, hipMemcpyDeviceToHost, c.s));
+      HIP_TRY(hipStreamSynchronize(c.s));
+      if (st) return st;
       uint64_t slot = 0;
       for (uint64_t i = 0; i < k; i++)
-        if (!original[i])
-          HIP_TRY(hipMemcpy(restored_out[i], static_cast<uint8_t *>(dout.p) + (slot++) * sb, sb,
-                            hipMemcpyDeviceToHost));
+        if (!original[i]) std::memcpy(restored_out[i], c.h + o_out + (slot++) * sb, sb);
     }
     for (uint64_t i = 0; i < k; i++)  // root.zig:76-81
       if (original[i]) std::memcpy(restored_out[i], original[i], sb);
