@@ -1494,7 +1494,11 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       ea.contig = contig_ok(sb, ke.nv);
       ea.skip = static_cast<const uint32_t *>(plan->skip->p);
       const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net, sb) : nullptr;
-      const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap * 4 / (m * sb)));
+      // scratch per slice (RS_AMD_SYN_SLICE_MB, default 4096): a slice whose syndromes fit
+      // the 256 MB Infinity Cache is read back by the map from there
+      const char *sl = std::getenv("RS_AMD_SYN_SLICE_MB");
+      const uint64_t cap = (sl && *sl ? std::max(1, std::atoi(sl)) : 4096) * (1ull << 20);
+      const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, cap / (m * sb)));
       void *scratch = nullptr;
       HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));
       for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
