@@ -184,6 +184,12 @@ int rs_reconstruct_batch_host_multi(uint64_t original_count, uint64_t recovery_c
 const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
 const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                        const uint8_t *present);
+/* Path rs_reconstruct_batch_dev_patterns takes for these arguments (16-byte aligned
+ * buffers): "psyn_k<k>_m<m>" (the code's syndrome network + per-stripe solve),
+ * "fft_syndromes+psyn_solve" (wide codes: FFT kernel with per-stripe masks + solve),
+ * "pattern_matrix" (per-stripe e x k table matrices) or "pattern_fft" (FFT kernels). */
+const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
+                                    uint32_t max_e, uint32_t flags);
 
 /* Large reconstruct network maps (the e x e syndrome map of wide codes, e.g. RS(200,55)
  * losing 55 data shards: ~16-36 s of hipRTC) compile in a background thread; until they are

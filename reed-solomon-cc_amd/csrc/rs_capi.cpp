@@ -1710,6 +1710,22 @@ bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
 
 }  // namespace
 
+const char *rs_patterns_kernel_name(uint64_t k, uint64_t m, size_t sb, uint32_t max_e, uint32_t flags) {
+  thread_local std::string name;
+  if (psyn_enabled(k, m, sb, flags)) {
+    name = "psyn_k" + std::to_string(k) + "_m" + std::to_string(m);
+  } else if (wps_enabled(k, m, sb, flags, max_e)) {
+    name = "fft_syndromes+psyn_solve";
+  } else {
+    const char *pm = std::getenv("RS_AMD_PATTERNS");
+    const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
+    const bool matrix =
+        !(flags & RS_FLAG_QUIRK_D1) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
+    name = matrix ? "pattern_matrix" : "pattern_fft";
+  }
+  return name.c_str();
+}
+
 int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const uint8_t *d_present,
                                       uint64_t present_stride, uint32_t max_e, const void *d_original,
                                       uint64_t orig_stride, const void *d_recovery, uint64_t rec_stride,

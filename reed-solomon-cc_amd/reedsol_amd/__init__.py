@@ -91,6 +91,7 @@ def lib():
         "rs_jit_stats": (C.c_int, [vp, vp, vp]),
         "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
         "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
+        "rs_patterns_kernel_name": (C.c_char_p, [u64, u64, sz, u32, u32]),
         "rs_fft_selftest": (C.c_int, [u64, u64, u32, vp, C.c_int, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
@@ -328,6 +329,11 @@ def reconstruct_batch_dev_patterns(original_count: int, recovery_count: int, pre
 
 def encode_kernel_name(k, m, shard_bytes) -> str:
     return lib().rs_encode_kernel_name(k, m, shard_bytes).decode()
+
+
+def patterns_kernel_name(k, m, shard_bytes, max_e, flags=0) -> str:
+    """Path of reconstruct_batch_dev_patterns for these arguments (include/reedsol.h)."""
+    return lib().rs_patterns_kernel_name(k, m, shard_bytes, max_e, flags).decode()
 
 
 def reconstruct_kernel_name(k, m, shard_bytes, present=None) -> str:

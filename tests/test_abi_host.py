@@ -204,6 +204,20 @@ def test_fft_kernel_compiles_for_gfx950(monkeypatch):
     assert R.fft_compile_check(32, 32)["code_bytes"] > 10000
 
 
+def test_patterns_path_selection(monkeypatch):
+    """rs_reconstruct_batch_dev_patterns' path per code (include/reedsol.h)."""
+    assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "psyn_k10_m4"
+    assert R.patterns_kernel_name(64, 4, 4096, 4) == "psyn_k64_m4"
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 8) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 9) == "pattern_fft"  # max_e > 8: no solve kernel
+    assert R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_matrix" or \
+        R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_fft"  # D1: no syndrome network
+    assert R.patterns_kernel_name(10, 4, 2048, 4) == "pattern_matrix"  # below the 4 KiB unit
+    assert R.patterns_kernel_name(5, 5, 4096, 5) == "pattern_matrix"
+    monkeypatch.setenv("RS_AMD_PATTERNS", "fft")
+    assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "pattern_fft"
+
+
 def test_psyn_kernel_compiles_for_gfx950():
     """Per-stripe syndrome network (rs_psyn.hpp): generated and compiled per code; codes
     outside its range (m > 4, D1 multiply, low rate) have none."""

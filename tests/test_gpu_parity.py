@@ -462,6 +462,7 @@ def test_per_stripe_syndrome_network(oracle, flags, max_e):
     syndrome network against the oracle, D2 schedule too; stripes losing more originals
     than max_e restore the first max_e and report RS_ERR_INVALID_ARGUMENT (14)."""
     k, m, sb, n = 10, 4, 65536, 37
+    assert R.patterns_kernel_name(k, m, sb, max_e, flags) == "psyn_k10_m4"
     rng = np.random.default_rng(1004 + flags + max_e)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
     par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
@@ -490,6 +491,7 @@ def test_per_stripe_wide_codes(oracle, k, m, sb, n, flags):
     originals (plus some recovery shards); more than 8 restore the first 8 and report 14;
     too few present report 2 and write nothing."""
     rng = np.random.default_rng(k * 7 + m + flags)
+    assert R.patterns_kernel_name(k, m, sb, 8, flags) == "fft_syndromes+psyn_solve"
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
     par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
     present = np.ones((n, k + m), np.uint8)
