@@ -928,7 +928,7 @@ const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pendin
       }
       return k;
     }
-    copy.prefetch = copy.prefetch > 2 ? 2 : 0;  // spilled: less prefetch (fewer live registers)
+    copy.prefetch = copy.prefetch > 3 ? 3 : copy.prefetch > 2 ? 2 : 0;  // spilled: less prefetch (fewer live registers)
   }
 }
 

@@ -204,6 +204,14 @@ def test_fft_kernel_compiles_for_gfx950(monkeypatch):
     assert R.fft_compile_check(32, 32)["code_bytes"] > 10000
 
 
+def test_shared_network_compiles_for_gfx950(monkeypatch):
+    """Two output tiles: the shared-input form (one workgroup of tile waves per unit,
+    inputs staged through LDS) is generated and compiles; so does the classic form."""
+    assert R.net_compile_check(16, 16) > 0
+    monkeypatch.setenv("RS_AMD_NET_SHARED", "0")
+    assert R.net_compile_check(16, 16) > 0
+
+
 def test_patterns_path_selection(monkeypatch):
     """rs_reconstruct_batch_dev_patterns' path per code (include/reedsol.h)."""
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "psyn_k10_m4"
