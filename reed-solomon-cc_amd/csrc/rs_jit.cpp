@@ -250,7 +250,7 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //                        -1: on above 16 input blocks; off costs nothing to compile
 //                        for small networks and measured ~1.5% faster on RS(10,4))
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, shared_batch = 1;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, shared_batch = 1, balance = 1;
 };
 
 int env_int(const char *name, int def) {
@@ -268,13 +268,15 @@ Tuning tuning() {
   t.tile = env_int("RS_AMD_NET_TILE", t.tile) >= 8 ? 8 : 4;
   t.shared = env_int("RS_AMD_NET_SHARED", t.shared);
   t.shared_batch = env_int("RS_AMD_NET_SHARED_BATCH", t.shared_batch);
+  t.balance = env_int("RS_AMD_NET_BALANCE", t.balance) != 0;
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
   return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt) + "b" +
          std::to_string(t.barrier) + "u" + std::to_string(t.units) + "t" + std::to_string(t.tile) + "s" +
-         std::to_string(t.shared) + (t.shared_batch != 1 ? "x" + std::to_string(t.shared_batch) : "");
+         std::to_string(t.shared) + (t.shared_batch != 1 ? "x" + std::to_string(t.shared_batch) : "") +
+         (t.balance ? "" : "nb");
 }
 
 // Shared-input form (generate_shared): one workgroup of n_tiles waves per 4 KiB unit,
@@ -286,6 +288,21 @@ std::string tuning_key(const Tuning &t) {
 bool shared_on(const Tuning &t, const NetSpec &spec) {
   const uint32_t n_tiles = (spec.n_out + t.tile - 1) / t.tile;
   return spec.pieces == 1 && n_tiles >= 2 && n_tiles <= 8 && t.shared != 0;
+}
+
+// Waves per workgroup of the shared form. Its ~200-VGPR waves fit two per SIMD, and a
+// workgroup's waves advance together (one barrier per batch), so a workgroup of 3 or
+// 5..7 waves leaves SIMDs holding one wave fewer than the others for the whole kernel
+// (7 waves: 2,2,2,1). RS_AMD_NET_BALANCE (default on) rounds the wave count up to 4 or
+// 8 and spreads the outputs evenly (55 outputs: 8 tiles of 7/6 instead of 7 of 8/7).
+uint32_t shared_tiles(const Tuning &t, const NetSpec &spec) {
+  const uint32_t n_tiles = (spec.n_out + t.tile - 1) / t.tile;
+  if (!t.balance) return n_tiles;
+  return n_tiles == 3 ? std::min(4u, spec.n_out) : n_tiles >= 5 ? std::min(8u, spec.n_out) : n_tiles;
+}
+
+uint32_t kernel_tiles(const Tuning &t, const NetSpec &spec) {
+  return shared_on(t, spec) ? shared_tiles(t, spec) : (spec.n_out + t.tile - 1) / t.tile;
 }
 
 }  // namespace
@@ -330,10 +347,11 @@ namespace {
 // is read from HBM and transposed once instead of once per tile.
 std::string generate_shared(const NetSpec &spec, const std::string &name, const Tuning &tu) {
   const uint32_t n_in = spec.n_in, n_out = spec.n_out;
-  const uint32_t tw = static_cast<uint32_t>(tu.tile);
   // RS_AMD_NET_SHARED_BATCH: inputs staged per wave between barriers (batch = T * mult)
   // (two buffers of 4 KiB per staged input within the 160 KiB of LDS)
-  const uint32_t T = (n_out + tw - 1) / tw;
+  const uint32_t T = shared_tiles(tu, spec);
+  // tile w owns outputs [w * n_out / T, (w + 1) * n_out / T)
+  auto tile_first = [&](uint32_t w) { return static_cast<uint32_t>(static_cast<uint64_t>(w) * n_out / T); };
   const uint32_t mult = std::max(1u, std::min({4u, static_cast<uint32_t>(std::max(1, tu.shared_batch)), 20u / T}));
   const uint32_t BW = T * mult, nb = (n_in + BW - 1) / BW;
   std::ostringstream o;
@@ -368,7 +386,7 @@ std::string generate_shared(const NetSpec &spec, const std::string &name, const 
   // merged the tiles' live ranges: 372 VGPRs and spills for RS(32,32)); every path
   // passes the same number of barriers.
   for (uint32_t tile = 0; tile < T; tile++) {
-    const uint32_t j0 = tile * tw, nj = std::min(tw, n_out - j0);
+    const uint32_t j0 = tile_first(tile), nj = tile_first(tile + 1) - j0;
     o << "  " << (tile ? "else if" : "if") << " (w == " << tile << "u) {\n  u32 ";
     for (size_t r = 0; r < 16 * nj; r++) o << "a" << r << (r + 1 < 16 * nj ? ", " : ";\n");
     std::vector<bool> init(16 * nj, false);
@@ -728,7 +746,7 @@ std::unique_ptr<Kernel> build(const NetSpec &spec, const std::string &key, const
   if (!k) return nullptr;
   k->n_in = spec.n_in;
   k->n_out = spec.n_out;
-  k->n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
+  k->n_tiles = kernel_tiles(tu, spec);
   k->units = static_cast<uint32_t>(tu.units);
   k->pieces = spec.pieces;
   k->shared = shared_on(tu, spec);
@@ -882,7 +900,7 @@ const Kernel *get_async(const NetSpec &spec, std::string &err, bool &pending) {
                       [spec, tu](Kernel &k) {
                         k.n_in = spec.n_in;
                         k.n_out = spec.n_out;
-                        k.n_tiles = (spec.n_out + tu.tile - 1) / tu.tile;
+                        k.n_tiles = kernel_tiles(tu, spec);
                         k.units = static_cast<uint32_t>(tu.units);
                         k.pieces = spec.pieces;
                         k.shared = shared_on(tu, spec);

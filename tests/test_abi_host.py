@@ -208,6 +208,10 @@ def test_shared_network_compiles_for_gfx950(monkeypatch):
     """Two output tiles: the shared-input form (one workgroup of tile waves per unit,
     inputs staged through LDS) is generated and compiles; so does the classic form."""
     assert R.net_compile_check(16, 16) > 0
+    # 24 outputs = 3 tiles of 8: four balanced waves of 6 (RS_AMD_NET_BALANCE), or three
+    assert R.net_compile_check(24, 24) > 0
+    monkeypatch.setenv("RS_AMD_NET_BALANCE", "0")
+    assert R.net_compile_check(24, 24) > 0
     monkeypatch.setenv("RS_AMD_NET_SHARED", "0")
     assert R.net_compile_check(16, 16) > 0
 

@@ -79,3 +79,25 @@ def test_encode_background_shared_network(oracle, monkeypatch, k, m):
         assert np.array_equal(enc(), exp)
     R.net_wait()
     assert np.array_equal(enc(), exp)
+
+
+@pytest.mark.parametrize("balance", ["1", "0"])
+@pytest.mark.parametrize("k,m,lost", [(64, 64, list(range(0, 64, 3))[:20] + list(range(1, 64, 3))[:20]),
+                                      (32, 24, list(range(0, 32, 2)) + [1, 3, 5])])
+def test_shared_reconstruct_balanced_waves(oracle, shared, monkeypatch, balance, k, m, lost):
+    """Maps of 3 and 5..7 output tiles: with RS_AMD_NET_BALANCE the workgroup runs 4 / 8
+    waves over evenly split outputs (40 outputs: 8 x 5; 19: 3 x 5 + 4), else 3 / 5 waves
+    of 8; both restore the erased data."""
+    monkeypatch.setenv("RS_AMD_NET_BALANCE", balance)
+    sb, n = 8192, 2
+    rng = np.random.default_rng(k + len(lost) + int(balance))
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=8)
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    d = torch.from_numpy(data).to(DEV)
+    d[:, lost] = 0
+    out = torch.zeros((n, len(lost), sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, d, torch.from_numpy(par).to(DEV), out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), data[:, lost]), R.reconstruct_kernel_name(k, m, sb, present)
