@@ -5,10 +5,12 @@ R=$(pwd); export TMPDIR=/tmp
 ARGS=${SWEEP_ARGS:---k 200 --m 55 --shard-bytes 262144 --stripes 64 --erase 0,2,4,6 --nv 2 --rounds 1 --reps 1}
 mkdir -p gpurun_out/sqw
 i=0
-for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD" \
-           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_WR"; do
+# PMC_GROUPS: counter groups separated by ';' (one rocprofv3 pass each)
+G=${PMC_GROUPS:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_WR"}
+IFS=';' read -ra GRPS <<< "$G"
+for grp in "${GRPS[@]}"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/sqw/g$i" -o run -- \
+  timeout -s KILL 150 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/sqw/g$i" -o run -- \
     python3 "$R/tools/kernel_sweep.py" $ARGS > gpurun_out/sqw/g$i.log 2>&1 || { echo "group $i failed"; tail -5 gpurun_out/sqw/g$i.log; exit 1; }
 done
 python3 - <<'PY'
