@@ -56,6 +56,48 @@ __global__ __launch_bounds__(256) void probe(const uint8_t *in, uint8_t *out, ui
   }
 }
 
+// unit4k: a wave covers a 4 KiB unit of every shard, four 16-B loads per lane 1 KiB apart
+// (the network kernels' pattern); one wave per unit, 4 waves per workgroup
+template <int K, int M, bool NT>
+__global__ __launch_bounds__(256) void probe4k(const uint8_t *in, uint8_t *out, uint64_t sb, uint64_t n) {
+  const uint64_t units = sb / 4096, lane = threadIdx.x & 63;
+  const uint64_t u = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (u >= units) return;
+  for (uint64_t s = blockIdx.y; s < n; s += gridDim.y) {
+    const uint8_t *src = in + s * K * sb + u * 4096 + lane * 16;
+    u4 a[4] = {};
+#pragma unroll
+    for (int i = 0; i < K; i++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) a[q] ^= ld<NT>(reinterpret_cast<const u4 *>(src + i * sb + q * 1024));
+    uint8_t *dst = out + s * M * sb + u * 4096 + lane * 16;
+    if (M == 0) {  // read-only shape: every loaded dword decides a (never taken) store
+      const u4 t = a[0] ^ a[1] ^ a[2] ^ a[3];
+      if ((t.x ^ t.y ^ t.z ^ t.w) == 0x9e3779b9u) st<NT>(reinterpret_cast<u4 *>(out + lane * 16), t);
+    }
+#pragma unroll
+    for (int j = 0; j < M; j++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) st<NT>(reinterpret_cast<u4 *>(dst + j * sb + q * 1024), a[q] + j);
+  }
+}
+
+template <int K, int M, bool NT>
+float run4k(const uint8_t *in, uint8_t *out, uint64_t sb, uint64_t n, int reps) {
+  dim3 grid((sb / 4096 + 3) / 4, n < 65535 ? n : 65535);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipLaunchKernelGGL((probe4k<K, M, NT>), grid, dim3(256), 0, 0, in, out, sb, n);
+  hipEventRecord(a);
+  for (int r = 0; r < reps; r++) hipLaunchKernelGGL((probe4k<K, M, NT>), grid, dim3(256), 0, 0, in, out, sb, n);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  return ms / reps;
+}
+
 template <int K, int M, bool SPLIT, bool NT>
 float run(const uint8_t *in, uint8_t *out, uint64_t sb, uint64_t n, int reps) {
   dim3 grid((sb / 32 + 255) / 256, n < 65535 ? n : 65535);
@@ -84,7 +126,20 @@ int main(int argc, char **argv) {
   } vs[] = {{"split  default", run<10, 4, true, false>},
             {"split  nt     ", run<10, 4, true, true>},
             {"contig default", run<10, 4, false, false>},
-            {"contig nt     ", run<10, 4, false, true>}};
+            {"contig nt     ", run<10, 4, false, true>},
+            {"unit4k default", run4k<10, 4, false>},
+            {"unit4k nt     ", run4k<10, 4, true>}};
+  struct V2 {
+    const char *name;
+    float (*f)(const uint8_t *, uint8_t *, uint64_t, uint64_t, int);
+  } shapes[] = {{"unit4k nt 14 read / 0 write", run4k<14, 0, true>},
+                {"unit4k nt 7 read / 7 write ", run4k<7, 7, true>}};
+  for (int round = 0; round < 2; round++)
+    for (auto &v : shapes) {
+      const float ms = v.f(in, out, sb, n / 2, 5);  // n/2 stripes of 14 shards fit both buffers
+      printf("{\"variant\": \"%s\", \"round\": %d, \"ms\": %.3f, \"TBps\": %.3f}\n", v.name, round, ms,
+             bytes / 2 / ms / 1e9);
+    }
   for (int round = 0; round < 3; round++)
     for (auto &v : vs) {
       const float ms = v.f(in, out, sb, n, 5);
