@@ -524,7 +524,12 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
   // batch, so its loads read zeros and its stores are dropped)
   const bool two = s.pieces == 2;
+  // RS_AMD_FFT_DEBUG_NOMEM (measurement aid, wrong bytes): bit 0 reads data through the
+  // zero-record resource (no load traffic), bit 1 drops the stores the same way
+  const int nomem = env_int("RS_AMD_FFT_DEBUG_NOMEM", 0);
   auto rsrc = [&](const char *base, const char *stride, const std::string &stripe, uint32_t rows) {
+    if (((nomem & 1) && std::string(base) == "data") || ((nomem & 2) && std::string(base) == "out"))
+      return std::string("RZ");
     return std::string("__builtin_amdgcn_make_buffer_rsrc((void *)(") + base + " + (" + stripe + ") * " + stride +
            "), (short)0, (int)(" + std::to_string(rows) + "u * sbl), 0x00020000)";
   };
@@ -881,7 +886,8 @@ std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft:p" + std::to_string(prefetch_of(s)) + "n" + std::to_string(nt_of()) + "s" +
                   std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 1)) +
-                  "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + "b" + std::to_string(blocked_of()) + ":" +
+                  "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + "b" + std::to_string(blocked_of()) +
+                  (env_int("RS_AMD_FFT_DEBUG_NOMEM", 0) ? "nomem" + std::to_string(env_int("RS_AMD_FFT_DEBUG_NOMEM", 0)) : "") + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
