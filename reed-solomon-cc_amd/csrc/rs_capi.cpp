@@ -1698,7 +1698,7 @@ bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t m
   const std::string mode = pm ? pm : "";
   return !(flags & RS_FLAG_QUIRK_D1) && (mode.empty() || mode == "auto" || mode == "psyn") && fft_enabled() &&
          fftnet::supports(k, m, sb) && fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
-         max_e <= psyn::kSolveMaxOut && m <= 64;
+         m <= 64;  // max_e up to m: output groups of 8 (rs_psyn.hpp launch_solve)
 }
 
 bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
@@ -1796,14 +1796,16 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       }
       if (fk && sk) {
         hipStream_t s = static_cast<hipStream_t>(stream);
-        const uint32_t dmw = fftnet::dyn_mask_words(*fs), pw = dmw + 2 + 64 + 64 * psyn::kSolveMaxOut;
+        // coefficients for min(max_e, m) outputs per syndrome, in groups of 8
+        const uint32_t cs = wps_coef_stride(static_cast<uint32_t>(std::min<uint64_t>(max_e, m)));
+        const uint32_t dmw = fftnet::dyn_mask_words(*fs), pw = dmw + 2 + 64 + 64 * cs;
         const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (m * sb)));
         void *blk = nullptr, *scratch = nullptr;
         HIP_TRY(hipMallocAsync(&blk, n_stripes * pw * sizeof(uint32_t), s));
         hipError_t e = hipMallocAsync(&scratch, per * m * sb, s);
         if (e == hipSuccess)
-          e = launch_wps_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m), max_e,
-                              n_stripes, static_cast<const uint16_t *>(pp->G->p), dexp, dlog, static_cast<uint32_t *>(blk),
+          e = launch_wps_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
+                              static_cast<uint32_t>(std::min<uint64_t>(max_e, m)), n_stripes, static_cast<const uint16_t *>(pp->G->p), dexp, dlog, static_cast<uint32_t *>(blk),
                               pw, dmw, d_status, s);
         for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += per) {
           const uint64_t cnt = std::min(per, n_stripes - s0);
@@ -1814,7 +1816,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
             e = psyn::launch_solve(*sk, static_cast<const uint8_t *>(d_recovery) + s0 * rec_stride, rec_stride,
                                    static_cast<const uint8_t *>(scratch), m * sb,
                                    static_cast<uint8_t *>(d_restored) + s0 * out_stride, out_stride, sb, cnt, bl, pw,
-                                   dmw, s);
+                                   dmw, cs, s);
         }
         if (scratch) (void)hipFreeAsync(scratch, s);
         (void)hipFreeAsync(blk, s);

@@ -134,7 +134,9 @@ hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uin
                             uint32_t *plan, uint32_t plan_dw, int32_t *status, hipStream_t s);
 
 // Per-stripe plan of the wide-code path: FFT mask block (dmw words) + solve header
-// (rs_kernels.hip k_wps_plan); plan_dw >= dmw + 2 + 64 + 64 * 8, m <= 64
+// (rs_kernels.hip k_wps_plan / k_wps_plan_wave); plan_dw >= dmw + 2 + 64 + 64 * cs,
+// cs = wps_coef_stride(max_e) (coefficients per syndrome: 8, or max_e rounded up to 8), m <= 64
+uint32_t wps_coef_stride(uint32_t max_e);
 hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_e,
                            uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log, uint32_t *plan,
                            uint32_t plan_dw, uint32_t dmw, int32_t *status, hipStream_t s);

@@ -1264,7 +1264,8 @@ __global__ __launch_bounds__(64) void k_psyn_plan(const uint8_t *__restrict__ pr
 // stripe (the e x 2e Gauss-Jordan lives in private memory). Block per stripe (u32):
 // [0, dmw) the FFT kernel's masks (fftnet::dyn_mask_words: erased data bits, then the
 // R rows stored), then at hdr = dmw: [0] outputs stored = min(e, max_e), [1] e,
-// [2, 2 + 64) R, [66 + i * 8 + j] = A^-1[j][i] in polynomial form for j < 8.
+// [2, 2 + 64) R, [66 + i * cs + j] = A^-1[j][i] in polynomial form for j < cs
+// (cs = wps_coef_stride(max_e): 8, or max_e rounded up to 8 for the wave kernel below).
 constexpr uint32_t kWpsMaxM = 64, kWpsMaxOut = 8;
 __global__ __launch_bounds__(64) void k_wps_plan(const uint8_t *__restrict__ present, uint64_t present_stride,
                                                  uint32_t k, uint32_t m, uint32_t max_e, uint64_t n,
@@ -1323,6 +1324,90 @@ __global__ __launch_bounds__(64) void k_wps_plan(const uint8_t *__restrict__ pre
   }
   hd[1] = e;
   hd[0] = e < max_e ? e : max_e;
+}
+
+// The same plan for max_e > 8 (every output of up to 64 erased originals): one wave per
+// stripe, the e x 2e Gauss-Jordan in LDS with the columns spread over the lanes (a
+// thread per stripe would run e^3 / 3 table multiplies on its own: ~55,000 for e = 55).
+// Coefficients at [66 + i * cs + j] for j < cs (cs = max_e rounded up to 8, <= 64).
+__global__ __launch_bounds__(64) void k_wps_plan_wave(const uint8_t *__restrict__ present, uint64_t present_stride,
+                                                      uint32_t k, uint32_t m, uint32_t max_e,
+                                                      const uint16_t *__restrict__ G, const uint16_t *__restrict__ exp,
+                                                      const uint16_t *__restrict__ log, uint32_t *__restrict__ plan,
+                                                      uint32_t plan_dw, uint32_t dmw, uint32_t cs,
+                                                      int32_t *__restrict__ status) {
+  __shared__ uint16_t A[kWpsMaxM][2 * kWpsMaxM];
+  __shared__ uint16_t E[kWpsMaxM], R[kWpsMaxM];
+  const uint64_t s = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const uint8_t *pr = present + s * present_stride;
+  uint32_t *pl = plan + s * plan_dw, *hd = pl + dmw;
+  uint32_t have = 0, e = 0;
+  for (uint32_t i = t; i < k + m; i += 64) {
+    have += pr[i] ? 1u : 0u;
+    e += (i < k && !pr[i]) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    have += __shfl_xor(have, o);
+    e += __shfl_xor(e, o);
+  }
+  if (t == 0 && status) status[s] = have < k ? 2 : (e > max_e ? 14 : 0);  // as k_pattern_tables
+  for (uint32_t i = t; i < dmw; i += 64) pl[i] = 0;
+  if (t == 0) hd[0] = hd[1] = 0;
+  if (have < k || e == 0 || e > kWpsMaxM) return;  // wave-uniform
+  if (t == 0) {
+    for (uint32_t i = 0, c = 0; i < k && c < e; i++)
+      if (!pr[i]) E[c++] = static_cast<uint16_t>(i);
+    for (uint32_t r = 0, c = 0; r < m && c < e; r++)
+      if (pr[k + r]) R[c++] = static_cast<uint16_t>(r);
+  }
+  __syncthreads();
+  for (uint32_t i = 0; i < e; i++)
+    for (uint32_t j = t; j < 2 * e; j += 64)
+      A[i][j] = static_cast<uint16_t>(j < e ? G[R[i] * k + E[j]] : (j - e == i ? 1u : 0u));
+  __syncthreads();
+  for (uint32_t c = 0; c < e; c++) {
+    const uint64_t nz = __ballot(t >= c && t < e && A[t][c] != 0);
+    if (nz == 0) return;  // singular: cannot happen for an MDS code (nothing restored)
+    const uint32_t piv = static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(nz)) - 1);
+    if (piv != c)
+      for (uint32_t j = t; j < 2 * e; j += 64) {
+        const uint16_t x = A[c][j];
+        A[c][j] = A[piv][j];
+        A[piv][j] = x;
+      }
+    __syncthreads();
+    const uint32_t inv = exp[(65535u - log[A[c][c]]) % 65535u];
+    __syncthreads();  // every lane has read the pivot before its column is scaled
+    for (uint32_t j = t; j < 2 * e; j += 64) A[c][j] = static_cast<uint16_t>(gf_mul_d(A[c][j], inv, exp, log));
+    __syncthreads();
+    for (uint32_t i = 0; i < e; i++) {
+      const uint32_t f = A[i][c];
+      __syncthreads();  // f read by every lane before the lane owning column c rewrites it
+      if (i != c && f)
+        for (uint32_t j = t; j < 2 * e; j += 64) A[i][j] ^= static_cast<uint16_t>(gf_mul_d(f, A[c][j], exp, log));
+    }
+    __syncthreads();
+  }
+  const uint16_t *cantor = G + m * k;
+  const uint32_t kw = dmw - 2;  // skip words, then 2 store words
+  if (t == 0)
+    for (uint32_t i = 0; i < e; i++) {
+      pl[E[i] / 32] |= 1u << (E[i] % 32);
+      pl[kw + R[i] / 32] |= 1u << (R[i] % 32);
+    }
+  for (uint32_t i = t; i < e; i += 64) hd[2 + i] = R[i];
+  for (uint32_t x = t; x < e * cs; x += 64) {
+    const uint32_t i = x / cs, j = x % cs;
+    const uint32_t c = j < e ? A[j][e + i] : 0u;
+    uint32_t poly = 0;
+    for (int b = 0; b < 16; b++) poly ^= (c >> b & 1u) ? cantor[b] : 0u;
+    hd[2 + kWpsMaxM + i * cs + j] = poly;
+  }
+  if (t == 0) {
+    hd[1] = e;
+    hd[0] = e < max_e ? e : max_e;
+  }
 }
 
 // The matrix path decodes from exactly k received shards (the present originals and
@@ -1747,15 +1832,25 @@ hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uin
   return hipGetLastError();
 }
 
+uint32_t wps_coef_stride(uint32_t max_e) {
+  return max_e <= kWpsMaxOut ? kWpsMaxOut : std::min(kWpsMaxM, (max_e + 7u) / 8u * 8u);
+}
+
 hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_e,
                            uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log, uint32_t *plan,
                            uint32_t plan_dw, uint32_t dmw, int32_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (m > kWpsMaxM || dmw < 2 || plan_dw < dmw + 2 + kWpsMaxM + kWpsMaxM * kWpsMaxOut ||
-      (dmw - 2) * 32 < k)
+  const uint32_t cs = wps_coef_stride(max_e);
+  if (m > kWpsMaxM || dmw < 2 || plan_dw < dmw + 2 + kWpsMaxM + kWpsMaxM * cs || (dmw - 2) * 32 < k)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_wps_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present, present_stride,
-                     k, m, max_e, n, G, d_exp, d_log, plan, plan_dw, dmw, status);
+  if (cs == kWpsMaxOut) {
+    hipLaunchKernelGGL(k_wps_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present,
+                       present_stride, k, m, max_e, n, G, d_exp, d_log, plan, plan_dw, dmw, status);
+  } else {
+    if (n > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_wps_plan_wave, dim3(static_cast<uint32_t>(n)), dim3(64), 0, s, present, present_stride, k, m,
+                       max_e, G, d_exp, d_log, plan, plan_dw, dmw, cs, status);
+  }
   return hipGetLastError();
 }
 

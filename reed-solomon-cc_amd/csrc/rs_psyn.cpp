@@ -217,14 +217,17 @@ std::string generate_solve(const uint16_t *cantor, const std::string &name) {
   o << "#define RS_NT 3\n" << jit::net_prelude();
   o << "extern \"C\" __global__ __launch_bounds__(256) void " << name
     << "(const unsigned char *__restrict__ rec, u64 rs, const unsigned char *__restrict__ scr, u64 ss,\n"
-       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0, const u32 *__restrict__ plan, u32 pw, u32 hdr) {\n"
+       "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0, const u32 *__restrict__ plan, u32 pw, u32 hdr,\n"
+       "    u32 cs) {\n"
        "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
        "  const u64 s = stripe0 + blockIdx.y;\n"
        "  const u64 unit = (u64)blockIdx.x * 4u + (threadIdx.x >> 6);\n"
        "  if (unit * 4096u >= sb) return;\n"
        "  const u32 *pl = plan + s * pw + hdr;\n"
-       "  const u32 ne = pl[0], e = pl[1];\n"
-       "  if (ne == 0u) return;\n"
+       // output group blockIdx.z: originals g8 .. g8 + 7 of the stripe's erased list
+       "  const u32 g8 = blockIdx.z * " << MO << "u, e = pl[1];\n"
+       "  if (pl[0] <= g8) return;\n"
+       "  const u32 ne = pl[0] - g8;\n"
        "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
        "  const unsigned char *RB = rec + s * rs, *SB = scr + s * ss;\n"
        "  unsigned char *O = out + s * so;\n";
@@ -247,7 +250,7 @@ std::string generate_solve(const uint16_t *cantor, const std::string &name) {
       if (!init[c]) o << "  a" << c << " = 0u;\n";
   }
   for (uint32_t j = 0; j < MO; j++) {
-    o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << 2 + 64 << "u + i * " << MO << "u + " << j << "u];\n  u32 ";
+    o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << 2 + 64 << "u + i * cs + g8 + " << j << "u];\n  u32 ";
     for (int c = 0; c < 16; c++) o << "X" << c << " = a" << c << (c == 15 ? ";\n" : ", ");
     emit_chain(o, j);
     o << "  }\n";
@@ -265,14 +268,14 @@ std::string generate_solve(const uint16_t *cantor, const std::string &name) {
       if (!init[c]) o << "  a" << c << " = 0u;\n";
     o << "  u32 Q[16] = {";
     for (int c = 0; c < 16; c++) o << "a" << c << (c == 15 ? "};\n" : ", ");
-    o << "  st(O + " << j << "ull * sb + off, Q);\n  }\n";
+    o << "  st(O + (u64)(g8 + " << j << "u) * sb + off, Q);\n  }\n";
   }
   o << "}\n";
   return o.str();
 }
 
 const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err) {
-  std::string key = "psolve:o" + std::to_string(kSolveMaxOut) + ":";
+  std::string key = "psolve:v2:o" + std::to_string(kSolveMaxOut) + ":";  // v2: output groups (blockIdx.z)
   key.append(reinterpret_cast<const char *>(cantor), 16 * sizeof(uint16_t));
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
@@ -297,9 +300,11 @@ bool compile_check_solve(const uint16_t *cantor, std::string &err, double *ms, s
 
 hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_, const uint8_t *scratch, uint64_t ss,
                         uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
-                        uint32_t plan_dw, uint32_t hdr, hipStream_t st) {
+                        uint32_t plan_dw, uint32_t hdr, uint32_t cs, hipStream_t st) {
   if (n_stripes == 0) return hipSuccess;
   if (sb == 0 || sb % jit::kUnitBytes || sb >= (1ull << 32)) return hipErrorInvalidValue;
+  if (cs == 0 || cs % kSolveMaxOut || cs > 64 || plan_dw < hdr + 2 + 64 + 64 * cs) return hipErrorInvalidValue;
+  const uint32_t groups = cs / kSolveMaxOut;
   const uint64_t gx = (sb / jit::kUnitBytes + 3) / 4;
   for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
     const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
@@ -307,9 +312,9 @@ hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_,
     unsigned char *o = out;
     uint64_t st0 = rs_, st1 = ss, so = so_, sbv = sb, first = s0;
     const uint32_t *pp = plan;
-    uint32_t pw = plan_dw, hd = hdr;
-    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sbv, &first, &pp, &pw, &hd};
-    hipError_t e = hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(gx), gy, 1, 256, 1, 1, 0, st, args, nullptr);
+    uint32_t pw = plan_dw, hd = hdr, c = cs;
+    void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sbv, &first, &pp, &pw, &hd, &c};
+    hipError_t e = hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(gx), gy, groups, 256, 1, 1, 0, st, args, nullptr);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -56,7 +56,8 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *orig, uin
                   uint64_t rs_, uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
                   hipStream_t st);
 
-// Wide codes (chunk 32 / 64, any e <= m <= 64; outputs <= kSolveMaxOut per stripe): the
+// Wide codes (chunk 32 / 64, any e <= m <= 64; outputs in groups of kSolveMaxOut, one
+// group per blockIdx.z, coefficient stride cs = 8 * groups): the
 // syndromes come from the bit-sliced FFT kernel with per-stripe masks (fftnet::Spec::dyn:
 // erased shards read as zero, only the rows R stored into a scratch), and one generic
 // kernel solves x = A^-1 (rec[R] ^ scratch[R]) with the alpha chains above, a runtime
@@ -68,7 +69,7 @@ const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err);
 bool compile_check_solve(const uint16_t *cantor, std::string &err, double *ms, size_t *code_bytes);
 hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_, const uint8_t *scratch, uint64_t ss,
                         uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
-                        uint32_t plan_dw, uint32_t hdr, hipStream_t st);
+                        uint32_t plan_dw, uint32_t hdr, uint32_t cs, hipStream_t st);
 
 }  // namespace psyn
 }  // namespace rs

@@ -221,7 +221,10 @@ def test_patterns_path_selection(monkeypatch):
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "psyn_k10_m4"
     assert R.patterns_kernel_name(64, 4, 4096, 4) == "psyn_k64_m4"
     assert R.patterns_kernel_name(200, 55, 1 << 18, 8) == "fft_syndromes+psyn_solve"
-    assert R.patterns_kernel_name(200, 55, 1 << 18, 9) == "pattern_fft"  # max_e > 8: no solve kernel
+    # max_e > 8: the solve runs in output groups of 8 (plan by one wave per stripe)
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 9) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 55) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(200, 55, 6144, 8) == "pattern_fft"  # no whole 4 KiB units
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_matrix" or \
         R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_fft"  # D1: no syndrome network
     assert R.patterns_kernel_name(10, 4, 2048, 4) == "pattern_matrix"  # below the 4 KiB unit

@@ -485,23 +485,24 @@ def test_per_stripe_syndrome_network(oracle, flags, max_e):
 @pytest.mark.parametrize("k,m,sb,n", [(200, 55, 8192, 13), (100, 20, 4096, 9), (33, 17, 4096, 7), (64, 64, 4096, 5),
                                       (40, 50, 8192, 6)])
 @pytest.mark.parametrize("flags", [0, 2])
-def test_per_stripe_wide_codes(oracle, k, m, sb, n, flags):
-    """Wide codes, per-stripe patterns, max_e = 8: syndromes on the FFT kernel with
-    per-stripe masks, then the generic e x e solve (rs_psyn.hpp). Stripes lose 0..12
-    originals (plus some recovery shards); more than 8 restore the first 8 and report 14;
-    too few present report 2 and write nothing."""
-    rng = np.random.default_rng(k * 7 + m + flags)
-    assert R.patterns_kernel_name(k, m, sb, 8, flags) == "fft_syndromes+psyn_solve"
+@pytest.mark.parametrize("max_e", [8, 20, 64])
+def test_per_stripe_wide_codes(oracle, k, m, sb, n, flags, max_e):
+    """Wide codes, per-stripe patterns: syndromes on the FFT kernel with per-stripe masks,
+    then the generic e x e solve (rs_psyn.hpp) in output groups of 8 (max_e > 8: the
+    plan's Gauss-Jordan runs one wave per stripe, k_wps_plan_wave). Stripes lose
+    0..max_e + 4 originals (at most m, plus some recovery shards); more than max_e restore
+    the first max_e and report 14; too few present report 2 and write nothing."""
+    rng = np.random.default_rng(k * 7 + m + flags + max_e)
+    assert R.patterns_kernel_name(k, m, sb, max_e, flags) == "fft_syndromes+psyn_solve"
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
     par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
     present = np.ones((n, k + m), np.uint8)
     for s in range(n - 1):
-        e = int(rng.integers(0, min(12, m) + 1))
+        e = int(rng.integers(0, min(max_e + 4, m, k) + 1))
         present[s, rng.choice(k, size=e, replace=False)] = 0
         present[s, k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
     present[n - 1, :] = 1
     present[n - 1, : m + 1] = 0  # not enough shards
-    max_e = 8
     out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
     status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
     R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
