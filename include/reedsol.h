@@ -186,7 +186,8 @@ const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recover
                                        const uint8_t *present);
 /* Path rs_reconstruct_batch_dev_patterns takes for these arguments (16-byte aligned
  * buffers): "psyn_k<k>_m<m>" (the code's syndrome network + per-stripe solve),
- * "fft_syndromes+psyn_solve" (wide codes: FFT kernel with per-stripe masks + solve),
+ * "fft_syndromes+psyn_solve" (wide codes, chunk 32 / 64, any max_e: FFT kernel with
+ * per-stripe masks + the e x e solve in output groups of 8),
  * "pattern_matrix" (per-stripe e x k table matrices) or "pattern_fft" (FFT kernels). */
 const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                     uint32_t max_e, uint32_t flags);
