@@ -1381,11 +1381,19 @@ __global__ __launch_bounds__(64) void k_wps_plan_wave(const uint8_t *__restrict_
     __syncthreads();  // every lane has read the pivot before its column is scaled
     for (uint32_t j = t; j < 2 * e; j += 64) A[c][j] = static_cast<uint16_t>(gf_mul_d(A[c][j], inv, exp, log));
     __syncthreads();
+    // elimination: lane t owns columns t and t + 64 and holds row t's factor; the logs of
+    // the pivot row's entries are looked up once per pivot, so each update is one
+    // independent exp lookup (no dependent table chain, no barrier per row)
+    const uint32_t fr = t < e ? A[t][c] : 0u, lfr = fr ? log[fr] : 0u;
+    const uint32_t p0 = t < 2 * e ? A[c][t] : 0u, p1 = t + 64 < 2 * e ? A[c][t + 64] : 0u;
+    const uint32_t lp0 = p0 ? log[p0] : 0u, lp1 = p1 ? log[p1] : 0u;
+    __syncthreads();  // column c read by every lane before its owner rewrites it
+#pragma unroll 4
     for (uint32_t i = 0; i < e; i++) {
-      const uint32_t f = A[i][c];
-      __syncthreads();  // f read by every lane before the lane owning column c rewrites it
-      if (i != c && f)
-        for (uint32_t j = t; j < 2 * e; j += 64) A[i][j] ^= static_cast<uint16_t>(gf_mul_d(f, A[c][j], exp, log));
+      const uint32_t f = __shfl(fr, static_cast<int>(i)), lf = __shfl(lfr, static_cast<int>(i));
+      if (i == c || f == 0) continue;  // wave-uniform
+      if (p0) A[i][t] ^= exp[add_mod_d(lf, lp0)];
+      if (p1) A[i][t + 64] ^= exp[add_mod_d(lf, lp1)];
     }
     __syncthreads();
   }
