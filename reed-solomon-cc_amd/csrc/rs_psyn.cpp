@@ -249,11 +249,27 @@ std::string generate_solve(const uint16_t *cantor, const std::string &name) {
     for (int c = 0; c < 16; c++)
       if (!init[c]) o << "  a" << c << " = 0u;\n";
   }
-  for (uint32_t j = 0; j < MO; j++) {
-    o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << 2 + 64 << "u + i * cs + g8 + " << j << "u];\n  u32 ";
-    for (int c = 0; c < 16; c++) o << "X" << c << " = a" << c << (c == 15 ? ";\n" : ", ");
-    emit_chain(o, j);
-    o << "  }\n";
+  // one alpha chain per syndrome shared by the group's outputs: step i XORs s * alpha^i
+  // into every output whose coefficient has bit i (the chain's 45 XORs once, not per output)
+  o << "  const u32 *cfp = pl + " << 2 + 64 << "u + i * cs + g8;\n";
+  for (uint32_t j = 0; j < MO; j++) o << "  const u32 cf" << j << " = " << j << "u < ne ? cfp[" << j << "] : 0u;\n";
+  o << "  u32 ";
+  for (int c = 0; c < 16; c++) o << "X" << c << " = a" << c << (c == 15 ? ";\n" : ", ");
+  {
+    std::vector<int> nm(16);
+    for (int c = 0; c < 16; c++) nm[c] = c;
+    for (int i = 0; i < 16; i++) {
+      for (uint32_t j = 0; j < MO; j++) {
+        o << "  if ((cf" << j << " >> " << i << ") & 1u) {";
+        for (int c = 0; c < 16; c++) o << " x" << j << "_" << c << " ^= X" << nm[c] << ";";
+        o << " }\n";
+      }
+      if (i == 15) break;
+      const int top = nm[15];
+      for (int c = 15; c > 0; c--) nm[c] = nm[c - 1];
+      nm[0] = top;
+      o << "  X" << nm[2] << " ^= X" << top << "; X" << nm[3] << " ^= X" << top << "; X" << nm[5] << " ^= X" << top << ";\n";
+    }
   }
   o << "  Rc = Rn;\n  }\n";
   for (uint32_t j = 0; j < MO; j++) {
@@ -275,7 +291,8 @@ std::string generate_solve(const uint16_t *cantor, const std::string &name) {
 }
 
 const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err) {
-  std::string key = "psolve:v2:o" + std::to_string(kSolveMaxOut) + ":";  // v2: output groups (blockIdx.z)
+  // v3: output groups (blockIdx.z), one alpha chain per syndrome
+  std::string key = "psolve:v3:o" + std::to_string(kSolveMaxOut) + ":";
   key.append(reinterpret_cast<const char *>(cantor), 16 * sizeof(uint16_t));
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
