@@ -716,11 +716,19 @@ bool enabled() {
 
 namespace {
 
+// set by the exit handler (Worker::push): a compile still in flight at process exit
+// does not load its module
+std::atomic<bool> g_exiting{false};
+
 // source -> loaded module; no lock held (compiles run concurrently)
 std::unique_ptr<Kernel> build_source(const std::string &name, const std::string &src, std::string &err) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
   if (!compile(src, code, err)) return nullptr;
+  if (g_exiting.load()) {
+    err = "process exiting";
+    return nullptr;
+  }
   auto k = std::make_unique<Kernel>();
   hipError_t e = hipModuleLoadData(&k->module, code.data());
   if (e != hipSuccess) {
@@ -769,9 +777,13 @@ const Kernel *insert(const std::string &key, std::unique_ptr<Kernel> k) {  // g_
   return out;
 }
 
-// One background worker compiles the queued maps in order. At unload it drops the
-// queue and finishes only the compile in flight; it is defined after the caches
-// above, so it is destroyed (joined) before them.
+// One background worker compiles the queued maps in order. At exit it drops the queue
+// and finishes only the compile in flight (without loading it). The first push
+// registers an exit handler that does this: registered after the HIP runtime was
+// initialised, it runs before the runtime's own teardown, so no worker thread is still
+// inside hipRTC / HIP calls while the runtime and this library are torn down (a
+// process that exited during a background compile used to crash in teardown). The
+// worker is defined after the caches above, so it is destroyed (joined) before them.
 struct Job {
   std::string key, name;
   std::function<std::string()> gen;  // the kernel source (generated on the worker)
@@ -787,8 +799,24 @@ struct Worker {
 
   void push(Job j) {  // g_mu held
     queue.push_back(std::move(j));
-    if (!th.joinable()) th = std::thread([this] { run(); });
+    if (!th.joinable()) {
+      static std::once_flag once;
+      std::call_once(once, [] { std::atexit(stop_at_exit); });
+      th = std::thread([this] { run(); });
+    }
     wake.notify_one();
+  }
+  static void stop_at_exit();
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      stop = true;
+      for (const Job &j : queue) g_pending.erase(j.key);
+      queue.clear();
+      g_cv.notify_all();
+    }
+    wake.notify_all();
+    if (th.joinable()) th.join();
   }
   void run() {
     for (;;) {
@@ -815,18 +843,13 @@ struct Worker {
       g_cv.notify_all();
     }
   }
-  ~Worker() {
-    {
-      std::lock_guard<std::mutex> lk(g_mu);
-      stop = true;
-      for (const Job &j : queue) g_pending.erase(j.key);
-      queue.clear();
-      g_cv.notify_all();
-    }
-    wake.notify_all();
-    if (th.joinable()) th.join();
-  }
+  ~Worker() { shutdown(); }
 } g_worker;
+
+void Worker::stop_at_exit() {
+  g_exiting.store(true);
+  g_worker.shutdown();
+}
 
 bool env_on(const char *name) {
   const char *e = std::getenv(name);

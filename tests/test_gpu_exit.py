@@ -1,0 +1,46 @@
+"""A process may exit while the background worker is still compiling a network
+(rs_jit.cpp Worker: its exit handler drops the queue and joins the compile in flight
+before the HIP runtime is torn down). Before that handler, such an exit crashed in
+teardown (SIGSEGV after the results were printed): the host-memory path of
+tools/e2e_bench.py on RS(200,55), reproduced here."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys, torch
+sys.path.insert(0, %r)
+import reedsol_amd as R
+k, m, sb, n = 200, 55, 1 << 18, 8
+torch.cuda.init()
+d = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8).pin_memory()
+p = torch.empty((n, m, sb), dtype=torch.uint8).pin_memory()
+R.encode_batch_host(k, m, d, p)
+present = [1] * (k + m)
+for i in (0, 3, 6, 9):
+    present[i] = 0
+out = torch.empty((n, 4, sb), dtype=torch.uint8).pin_memory()
+for _ in range(3):  # the 200 -> 4 map (200 blocks) goes to the background worker
+    R.reconstruct_batch_host(k, m, present, d, p, out)
+assert torch.equal(out, d[:, [0, 3, 6, 9]])
+print("child done", flush=True)
+"""
+
+
+def test_exit_during_background_compile(tmp_path):
+    env = dict(os.environ, RS_AMD_CACHE_DIR=str(tmp_path))  # empty disk cache: the compile is in flight at exit
+    env.pop("RS_AMD_JIT_SYNC", None)
+    r = subprocess.run([sys.executable, "-c", CHILD % os.path.join(ROOT, "reed-solomon-cc_amd")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert "child done" in r.stdout, r.stderr[-2000:]
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
