@@ -798,6 +798,11 @@ struct Worker {
   bool stop = false;
 
   void push(Job j) {  // g_mu held
+    if (stop) {  // after the exit handler: nothing compiles any more (the caller keeps its table kernel)
+      g_pending.erase(j.key);
+      g_failed.emplace(j.key, "process exiting");
+      return;
+    }
     queue.push_back(std::move(j));
     if (!th.joinable()) {
       static std::once_flag once;
