@@ -500,9 +500,10 @@ uint64_t fft_encode_mul_count(uint64_t k, uint64_t m) {
 // losing 20 5.21 vs 3.90 ms, losing 14 3.56 vs 3.54, losing 8 2.61 vs 3.26 ms
 // (profiles/r02/sweep_direct_vs_syndrome.jsonl), hence the n_in * e bound.
 bool syndrome_pick(uint64_t k, uint64_t m, uint64_t e, uint32_t flags, uint64_t sb, const std::string &mode);
-bool direct_net_async(uint64_t e, uint64_t n_in, uint64_t sb, const std::string &mode, uint64_t k, uint64_t m) {
+bool direct_net_async(uint64_t e, uint64_t n_in, uint64_t sb, const std::string &mode, uint64_t k, uint64_t m,
+                      uint32_t flags) {
   if (mode == "auto" && fft_enabled() && fftnet::supports(k, m, sb) && n_in * e >= 2800 &&
-      syndrome_pick(k, m, e, 0, sb, mode))
+      syndrome_pick(k, m, e, flags, sb, mode))
     return false;
   return (mode == "auto" || mode == "net") && jit::enabled() &&
          !jit::supports(static_cast<uint32_t>(n_in), static_cast<uint32_t>(e), sb) &&
@@ -608,7 +609,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
   // past the synchronous cap: the same map compiled in the background, the matrix
   // kernel meanwhile (RS(200,55) losing 8: 400 blocks, against syndrome + encode)
-  const bool use_net_async = !use_net && kind != 0 && direct_net_async(e, n_in_want, sb, mode, k, m);
+  const bool use_net_async = !use_net && kind != 0 && direct_net_async(e, n_in_want, sb, mode, k, m, flags);
   const bool use_syn = !use_net && !use_net_async && syndrome_pick(k, m, e, flags, sb, mode);
   if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
   // the syndromes' e x e map as a network too (its table kernel stays the fallback)
@@ -623,7 +624,9 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   // every original lost and every recovery shard present, k == m == chunk: the data are
   // FFT_C(IFFT_0(recovery)) (rs_fftnet.hpp Spec::inverse); the plan's other kernels stay
   // the fallback
-  if (e == k && present_count == m && (mode == "auto" || mode == "net") && fft_enabled() &&
+  // (corrected multiply only: under D1 the literal reconstruct is no inverse of the encode,
+  // so its output is not the data and must follow root.zig:268-335 as written)
+  if (e == k && present_count == m && !d1 && (mode == "auto" || mode == "net") && fft_enabled() &&
       fftnet::supports_inverse(k, m, sb)) {
     plan->inv_fft = std::make_shared<FftSlot>();
     plan->inv_fft->spec.k = static_cast<uint32_t>(k);
@@ -1136,7 +1139,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
     return net_name("reconstruct", k, e);
-  if (decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode, k, m))
+  if (decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode, k, m, flags_none()))
     return net_name("reconstruct", k, e);
   if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
     thread_local std::string name;
@@ -1693,19 +1696,28 @@ void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<W
   out = p;
 }
 
+// Under D2 a code with k > chunk and k % chunk == 0 drops its last full chunk
+// (root.zig:151): the encode ignores those shards, the code is not MDS, and the
+// per-stripe e x e solves can be singular. Such codes take the FFT kernels, which
+// follow root.zig:268-335 as written.
+bool d2_drops_chunk(uint64_t k, uint64_t m, uint32_t flags) {
+  const uint64_t C = ceil_pow2(m);
+  return (flags & RS_FLAG_QUIRK_D2) && k > C && k % C == 0;
+}
+
 bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t max_e) {
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
-  return !(flags & RS_FLAG_QUIRK_D1) && (mode.empty() || mode == "auto" || mode == "psyn") && fft_enabled() &&
-         fftnet::supports(k, m, sb) && fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
+  return !(flags & RS_FLAG_QUIRK_D1) && !d2_drops_chunk(k, m, flags) &&
+         (mode.empty() || mode == "auto" || mode == "psyn") && fft_enabled() && fftnet::supports(k, m, sb) && fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
          m <= 64;  // max_e up to m: output groups of 8 (rs_psyn.hpp launch_solve)
 }
 
 bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
-  return !(flags & RS_FLAG_QUIRK_D1) && (mode.empty() || mode == "auto" || mode == "psyn") && jit::enabled() &&
-         psyn::supports(k, m, sb);
+  return !(flags & RS_FLAG_QUIRK_D1) && !d2_drops_chunk(k, m, flags) &&
+         (mode.empty() || mode == "auto" || mode == "psyn") && jit::enabled() && psyn::supports(k, m, sb);
 }
 
 }  // namespace

@@ -617,6 +617,15 @@ std::string cache_path(const std::string &dir, const std::string &src, const cha
   return dir + name;
 }
 
+// A code object is an ELF (or a clang offload bundle); anything else (a truncated or
+// foreign file) is not loaded.
+bool code_object_ok(const std::vector<char> &code) {
+  static const char kElf[4] = {0x7F, 'E', 'L', 'F'};
+  static const char kBundle[] = "__CLANG_OFFLOAD_BUNDLE__";
+  if (code.size() >= 64 && std::memcmp(code.data(), kElf, 4) == 0) return true;
+  return code.size() >= sizeof kBundle && std::memcmp(code.data(), kBundle, sizeof kBundle - 1) == 0;
+}
+
 bool cache_read(const std::string &path, std::vector<char> &code) {
   FILE *f = std::fopen(path.c_str(), "rb");
   if (!f) return false;
@@ -629,6 +638,10 @@ bool cache_read(const std::string &path, std::vector<char> &code) {
     ok = std::fread(code.data(), 1, code.size(), f) == code.size();
   }
   std::fclose(f);
+  if (ok && !code_object_ok(code)) {  // a bad entry is dropped and recompiled
+    std::remove(path.c_str());
+    ok = false;
+  }
   return ok;
 }
 
@@ -646,18 +659,26 @@ void cache_write(const std::string &dir, const std::string &path, const std::vec
   const std::string tmp = path + tmp_suffix;
   FILE *f = std::fopen(tmp.c_str(), "wb");
   if (!f) return;
-  const bool ok = std::fwrite(code.data(), 1, code.size(), f) == code.size();
-  std::fclose(f);
+  // published only when every byte reached the file (a full disk fails at write, flush or close)
+  bool ok = std::fwrite(code.data(), 1, code.size(), f) == code.size();
+  ok = std::fflush(f) == 0 && ok;
+  ok = ::fsync(::fileno(f)) == 0 && ok;
+  ok = std::fclose(f) == 0 && ok;
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());  // atomic publish
 }
 
 // hipRTC: source -> gfx950 code object (needs no device), through the disk cache
-bool compile(const std::string &src, std::vector<char> &code, std::string &err) {
+// *cached: the code came from the disk cache (whose entry a failed load then drops:
+// cache_drop); no_cache_read: compile even if an entry exists.
+bool compile(const std::string &src, std::vector<char> &code, std::string &err, std::string *cached = nullptr,
+             bool no_cache_read = false) {
   // -O1/-O2 measured no faster to compile (the time is in the backend)
   const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
   const std::string dir = cache_dir();
   const std::string path = dir.empty() ? std::string() : cache_path(dir, src, opts, 3);
-  if (!path.empty() && cache_read(path, code)) {
+  if (cached) cached->clear();
+  if (!path.empty() && !no_cache_read && cache_read(path, code)) {
+    if (cached) *cached = path;
     g_disk_hits++;
     if (std::getenv("RS_AMD_JIT_VERBOSE")) std::fprintf(stderr, "[rs_amd jit] code-object cache hit %s\n", path.c_str());
     return true;
@@ -724,13 +745,19 @@ std::atomic<bool> g_exiting{false};
 std::unique_ptr<Kernel> build_source(const std::string &name, const std::string &src, std::string &err) {
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<char> code;
-  if (!compile(src, code, err)) return nullptr;
+  std::string cached;
+  if (!compile(src, code, err, &cached)) return nullptr;
   if (g_exiting.load()) {
     err = "process exiting";
     return nullptr;
   }
   auto k = std::make_unique<Kernel>();
   hipError_t e = hipModuleLoadData(&k->module, code.data());
+  if (e != hipSuccess && !cached.empty()) {  // a bad disk-cache entry: drop it, compile once more
+    std::remove(cached.c_str());
+    if (!compile(src, code, err, nullptr, true)) return nullptr;
+    e = hipModuleLoadData(&k->module, code.data());
+  }
   if (e != hipSuccess) {
     err = std::string("hipModuleLoadData: ") + hipGetErrorString(e);
     return nullptr;

@@ -1228,7 +1228,10 @@ __global__ __launch_bounds__(64) void k_psyn_plan(const uint8_t *__restrict__ pr
   for (uint32_t c = 0; c < e; c++) {
     uint32_t piv = c;
     while (piv < e && A[piv][c] == 0) piv++;
-    if (piv == e) return;  // singular: cannot happen for an MDS code (nothing restored)
+    if (piv == e) {  // singular: not an MDS code (the host keeps such codes off this path)
+      if (status) status[s] = 15;  // RS_ERR_DEVICE: nothing restored
+      return;
+    }
     for (uint32_t j = 0; j < 2 * e; j++) {
       const uint32_t t = A[c][j];
       A[c][j] = A[piv][j];
@@ -1295,7 +1298,11 @@ __global__ __launch_bounds__(64) void k_wps_plan(const uint8_t *__restrict__ pre
   for (uint32_t c = 0; c < e; c++) {
     uint32_t piv = c;
     while (piv < e && A[piv][c] == 0) piv++;
-    if (piv == e) return;  // singular: cannot happen for an MDS code (nothing restored)
+    if (piv == e) {  // singular: not an MDS code (the host keeps such codes off this path)
+      if (status) status[s] = 15;  // RS_ERR_DEVICE: nothing restored
+      hd[0] = 0;
+      return;
+    }
     for (uint32_t j = 0; j < 2 * e; j++) {
       const uint16_t t = A[c][j];
       A[c][j] = A[piv][j];
@@ -1368,7 +1375,11 @@ __global__ __launch_bounds__(64) void k_wps_plan_wave(const uint8_t *__restrict_
   __syncthreads();
   for (uint32_t c = 0; c < e; c++) {
     const uint64_t nz = __ballot(t >= c && t < e && A[t][c] != 0);
-    if (nz == 0) return;  // singular: cannot happen for an MDS code (nothing restored)
+    if (nz == 0) {  // singular: not an MDS code (the host keeps such codes off this path)
+      if (t == 0 && status) status[s] = 15;  // RS_ERR_DEVICE: nothing restored
+      if (t == 0) hd[0] = 0;
+      return;
+    }
     const uint32_t piv = static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(nz)) - 1);
     if (piv != c)
       for (uint32_t j = t; j < 2 * e; j += 64) {

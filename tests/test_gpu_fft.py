@@ -133,3 +133,27 @@ def test_fft_inverse_reconstruct_all_originals(oracle, k, sb, n):
     got = out.cpu().numpy()
     assert np.array_equal(got[:n], data)
     assert (got[n] == 7).all()
+
+
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("flags", [1, 3])
+def test_fft_inverse_not_taken_under_d1(oracle, k, flags):
+    """Under D1 the literal reconstruct (root.zig:268-335 with Generic.zig:283's multiply)
+    is not the inverse of the encode, so every-original-lost must follow the reference's
+    decode as written, not the inverted encode: compare with the oracle's reconstruct."""
+    sb, n = 4096, 2
+    rng = np.random.default_rng(k + flags)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, k, data, quirks=flags, threads=8)
+    present = np.ones(2 * k, np.uint8)
+    present[:k] = 0
+    d = torch.zeros((n, k, sb), dtype=torch.uint8, device=DEV)
+    pr = torch.from_numpy(par).to(DEV)
+    out = torch.zeros((n, k, sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, k, present, d, pr, out, flags)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for s in range(n):
+        exp = oracle.reconstruct_batch(k, k, present, np.concatenate([data[s:s + 1], par[s:s + 1]], axis=1),
+                                       quirks=flags)
+        assert np.array_equal(got[s], exp[0]), s
