@@ -1,0 +1,220 @@
+// rs_common.cpp — errors, device checks, validation (root.zig:397-415 and the
+// Encoder/Decoder init checks), plan-cache plumbing, kernel slots, and the info ABI.
+#include "rs_host.hpp"
+
+namespace rs {
+namespace host {
+
+thread_local std::string t_last_error;
+
+int fail(int status, const std::string &msg) {
+  t_last_error = msg;
+  return status;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  return fail(RS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+
+const char *last_error() { return t_last_error.c_str(); }
+
+// ---------------------------------------------------------------- devices
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_ok;  // device -> RS_OK / RS_ERR_NO_DEVICE
+
+int current_device(int *dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RS_ERR_NO_DEVICE, "no HIP device visible");
+  HIP_TRY(hipGetDevice(dev));
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto it = g_dev_ok.find(*dev);
+  if (it == g_dev_ok.end()) {
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, *dev));
+    const bool ok = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    it = g_dev_ok.emplace(*dev, ok ? RS_OK : RS_ERR_NO_DEVICE).first;
+    if (!ok) return fail(RS_ERR_NO_DEVICE, std::string("device arch ") + prop.gcnArchName + " is not gfx950");
+  }
+  if (it->second != RS_OK) return fail(it->second, "device is not gfx950");
+  return RS_OK;
+}
+
+// ------------------------------------------------------------ validation
+// root.zig:397-415
+int use_high_rate(uint64_t original, uint64_t recovery) {
+  if (original > kOrder || recovery > kOrder) return -RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (original == 0 || recovery == 0) return -RS_ERR_UNSUPPORTED_SHARD_COUNT;  // ceilPowerOfTwo(0) asserts
+  const uint64_t op = ceil_pow2(original), rp = ceil_pow2(recovery);
+  const uint64_t smaller = std::min(op, rp), larger = std::max(original, recovery);
+  if (smaller + larger > kOrder) return -RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (op < rp) return 0;
+  if (op > rp) return 1;
+  return original <= recovery ? 1 : 0;
+}
+
+// Low rate runs as maps of k x m GF(2^16) constants (passes of <= 64 outputs): the
+// map size bounds the tables (96 B per entry) and the reconstruct's 16e x 16e solve.
+constexpr uint64_t kLowRateMaxMap = 1ull << 16;
+inline bool low_rate_ok(uint64_t k, uint64_t m) { return k * m <= kLowRateMaxMap; }
+
+// Encoder.init / Decoder.init checks (root.zig:100-103, 198-201) + the tail panic (root.zig:385)
+int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
+  const int hr = use_high_rate(k, m);
+  if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
+  // low rate: the reference panics (root.zig:120); here maps with k * m <= 65536 (§8 f4)
+  if (hr == 0 && !low_rate_ok(k, m))
+    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec with original_count * recovery_count > 65536");
+  if (shard_bytes == 0 || (shard_bytes & 1)) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes is 0 or odd");
+  // shard_bytes % 64 != 0: the reference panics (root.zig:385); handled here with
+  // the tail layout of root.zig:338-348 (tail_* below).
+  return RS_OK;
+}
+
+int align_nv(std::initializer_list<uint64_t> vals) {
+  uint64_t a = 0;
+  for (uint64_t v : vals) a |= v;
+  if (a % 16 == 0) return 4;
+  if (a % 8 == 0) return 2;
+  if (a % 4 == 0) return 1;
+  return 0;
+}
+
+uint32_t async_after() {
+  const char *e = std::getenv("RS_AMD_NET_ASYNC_AFTER");
+  return e && *e ? static_cast<uint32_t>(std::max(1, std::atoi(e))) : 2u;
+}
+
+// A fallback to the table kernels is reported on stderr once per distinct reason.
+void warn_once_per_reason(const char *what, const std::string &err) {
+  static std::mutex mu;
+  static std::set<std::string> seen;
+  std::lock_guard<std::mutex> lk(mu);
+  if (seen.insert(err.substr(0, 200)).second) std::fprintf(stderr, "%s%s\n", what, err.c_str());
+}
+
+bool fft_enabled() {
+  const char *e = std::getenv("RS_AMD_FFT");
+  return jit::enabled() && !(e && std::strcmp(e, "0") == 0);
+}
+
+// The slot's kernel for shards of sb bytes; *used = the spec to launch it with.
+const jit::Kernel *fft_kernel(FftSlot &slot, uint64_t sb, const fftnet::Spec **used) {
+  std::lock_guard<std::mutex> lk(slot.mu);
+  const int vi = fftnet::pieces(sb) > 1 ? 1 : 0;
+  if (slot.failed[vi]) return nullptr;
+  if (vi && slot.spec_p2.pieces == 1) {
+    slot.spec_p2 = slot.spec;
+    slot.spec_p2.pieces = 2;
+  }
+  const fftnet::Spec &spec = vi ? slot.spec_p2 : slot.spec;
+  *used = &spec;
+  std::string err;
+  bool pending = false;
+  const char *a = std::getenv("RS_AMD_FFT_ASYNC");
+  const bool async = a && *a ? std::strcmp(a, "0") != 0 : slot.async;
+  const jit::Kernel *k = fftnet::get(spec, async, err, pending);
+  if (!k && !pending) {
+    slot.failed[vi] = true;
+    warn_once_per_reason("[rs_amd] bit-sliced FFT kernel unavailable, using table kernels: ", err);
+  }
+  return k;
+}
+
+// Compile (once) and return the plan's network kernel; nullptr if hipRTC failed
+// (the caller then runs the precompiled table-driven kernels).
+// (jit::get caches by content and code-shape knobs; a failure is reported once per plan.)
+// An async slot returns nullptr (table kernels) until its background compile is done.
+// 1 / 2 KiB shards run a variant whose wave units span 4 / 2 stripes (jit::net_pieces).
+const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
+  std::lock_guard<std::mutex> lk(slot.mu);
+  const uint32_t pieces = jit::net_pieces(sb);
+  const int vi = pieces >= 4 ? 2 : pieces >= 2 ? 1 : 0;  // a failed variant does not disable the others
+  if (slot.failed[vi]) return nullptr;
+  std::string err;
+  bool pending = false;
+  if (slot.async && slot.uses < async_after()) {  // a one-off pattern is not worth a background compile
+    const char *sync = std::getenv("RS_AMD_JIT_SYNC");
+    if (!(sync && *sync && std::strcmp(sync, "0") != 0) && ++slot.uses < async_after()) return nullptr;
+  }
+  jit::NetSpec small;
+  if (pieces > 1) {
+    small = slot.spec;
+    small.pieces = pieces;
+  }
+  const jit::NetSpec &spec = pieces > 1 ? small : slot.spec;
+  const jit::Kernel *k = slot.async ? jit::get_async(spec, err, pending) : jit::get(spec, err);
+  if (!k && !pending) {
+    slot.failed[vi] = true;
+    warn_once_per_reason("[rs_amd] bit-sliced network unavailable, using table kernels: ", err);
+  }
+  return k;
+}
+
+std::mutex g_plan_mu;
+
+int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out) {
+  auto b = std::make_shared<DevBuf>();
+  b->dev = dev;
+  HIP_TRY(hipMalloc(&b->p, std::max<size_t>(bytes, 16)));
+  HIP_TRY(hipMemcpy(b->p, host, bytes, hipMemcpyHostToDevice));
+  out = b;
+  return RS_OK;
+}
+
+}  // namespace host
+}  // namespace rs
+
+using namespace rs;
+using namespace rs::host;
+
+extern "C" {
+
+const char *rs_version(void) { return "rs-amd 0.1.0 (gfx950)"; }
+
+const char *rs_status_name(int s) {
+  static const char *kNames[] = {"Ok",
+                                 "TooFewOriginalShards",
+                                 "NotEnoughShards",
+                                 "InvalidShardSize",
+                                 "UnsupportedShardCount",
+                                 "TooManyOriginalShards",
+                                 "DifferentShardSize",
+                                 "InvalidShardIndex",
+                                 "DuplicateShardIndex",
+                                 "TooManyShards",
+                                 "OutOfMemory",
+                                 "Overflow",
+                                 "LowRateUnsupported",
+                                 "ShardTailUnsupported",
+                                 "InvalidArgument",
+                                 "DeviceError",
+                                 "NoDevice"};
+  if (s < 0 || s >= static_cast<int>(sizeof kNames / sizeof kNames[0])) return "Unknown";
+  return kNames[s];
+}
+
+const char *rs_last_error(void) { return last_error(); }
+
+int rs_use_high_rate(uint64_t k, uint64_t m) { return use_high_rate(k, m); }
+
+const uint16_t *rs_table_exp(void) { return tables().exp; }
+const uint16_t *rs_table_log(void) { return tables().log; }
+const uint16_t *rs_table_skew(void) { return tables().skew; }
+const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
+
+int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules) {
+  return guarded([&]() -> int {
+    jit::compile_stats(compiles, cache_hits, modules);
+    return RS_OK;
+  });
+}
+
+int rs_net_wait(void) {
+  return guarded([&]() -> int {
+    jit::wait_pending();
+    return RS_OK;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,216 @@
+// rs_host.hpp — internal interface of the host codec (librs_amd.so): validation and
+// error reporting, plan caches, kernel selection, plans, and the entry points the
+// C ABI files (rs_batch_dev.cpp, rs_patterns.cpp, rs_lowrate.cpp, rs_host_batch.cpp,
+// rs_oneshot.cpp) share. Host-side mirror of root.zig's checks and error
+// precedence; every device computation runs in rs_kernels.hip or in a hipRTC
+// kernel (rs_jit / rs_fftnet / rs_psyn); there is no CPU compute path.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/reedsol.h"
+#include "rs_fftnet.hpp"
+#include "rs_gf.hpp"
+#include "rs_internal.hpp"
+#include "rs_jit.hpp"
+#include "rs_psyn.hpp"
+
+namespace rs {
+namespace host {
+
+// ------------------------------------------------------------ errors (rs_common.cpp)
+int fail(int status, const std::string &msg);  // sets rs_last_error()
+int hip_fail(hipError_t e, const char *what);
+const char *last_error();
+
+#define HIP_TRY(expr)                               \
+  do {                                              \
+    hipError_t e_ = (expr);                         \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+
+// No C++ exception may cross the C ABI: host allocation failures become
+// RS_ERR_OUT_OF_MEMORY, anything else RS_ERR_DEVICE with its message.
+template <class F>
+int guarded(F &&f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc &) {
+    return fail(RS_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception &ex) {
+    return fail(RS_ERR_DEVICE, ex.what());
+  } catch (...) {
+    return fail(RS_ERR_DEVICE, "unexpected exception");
+  }
+}
+
+// ---------------------------------------------------- validation (rs_common.cpp)
+int current_device(int *dev);  // RS_ERR_NO_DEVICE unless the current device is gfx950
+// root.zig:397-415: 1 high rate, 0 low rate, -status on invalid counts
+int use_high_rate(uint64_t original, uint64_t recovery);
+inline bool is_low_rate(uint64_t k, uint64_t m) { return use_high_rate(k, m) == 0; }
+// Encoder.init / Decoder.init checks (root.zig:100-103, 198-201)
+int check_codec(uint64_t k, uint64_t m, size_t shard_bytes);
+// widest per-lane access (4, 2, 1 dword pairs) the alignment of every value allows; 0 = none
+int align_nv(std::initializer_list<uint64_t> vals);
+
+// ------------------------------------------------------- plans (rs_common.cpp)
+struct DevBuf {
+  void *p = nullptr;
+  int dev = 0;
+  ~DevBuf() {
+    if (p) {
+      int cur = 0;
+      (void)hipGetDevice(&cur);
+      (void)hipSetDevice(dev);
+      (void)hipFree(p);
+      (void)hipSetDevice(cur);
+    }
+  }
+};
+
+// Bit-sliced network kernel of a plan (rs_jit.hpp), compiled on first use.
+struct NetSlot {
+  std::mutex mu;
+  bool failed[3] = {false, false, false};  // per variant: 4 KiB units, 2 / 4 stripes per unit (small shards)
+  bool async = false;  // past the synchronous size cap: compiled in the background
+  uint32_t uses = 0;   // async: the compile starts at the RS_AMD_NET_ASYNC_AFTER-th use (default 2)
+  jit::NetSpec spec;
+};
+
+uint32_t async_after();  // RS_AMD_NET_ASYNC_AFTER
+// A fallback to the table kernels is reported on stderr once per distinct reason.
+void warn_once_per_reason(const char *what, const std::string &err);
+
+// Bit-sliced FFT kernel of a plan (rs_fftnet.hpp): wide codes, compiled on first use.
+struct FftSlot {
+  std::mutex mu;
+  bool failed[2] = {false, false};  // per variant: 2 KiB units of one stripe / of two 1 KiB stripes
+  bool async = false;  // per-pattern kernels: background compile, the table encode meanwhile
+  fftnet::Spec spec;
+  fftnet::Spec spec_p2;  // the 1 KiB-shard variant (Spec::pieces 2), filled on first use
+};
+
+bool fft_enabled();
+// The slot's kernel for shards of sb bytes; *used = the spec to launch it with.
+const jit::Kernel *fft_kernel(FftSlot &slot, uint64_t sb, const fftnet::Spec **used);
+// The slot's network kernel (compiled on first use; nullptr: table kernels)
+const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb);
+
+struct EncodePlan {
+  std::shared_ptr<DevBuf> buf;
+  uint32_t chunk, n_chunks, trunc_first, trunc_last, tabs_per_chunk, work;
+  std::shared_ptr<NetSlot> net = std::make_shared<NetSlot>();
+  std::shared_ptr<FftSlot> fft;  // wide codes (chunk 32 / 64)
+};
+
+struct DecodePlan {
+  std::shared_ptr<DevBuf> buf;
+  bool matrix = false;
+  bool tiled = false;
+  uint32_t work = 0, chunk = 0, trunc = 0, e = 0, n_in = 0;
+  size_t off_fft = 0, off_pre = 0, off_post = 0, off_src = 0, off_dst = 0, off_mat = 0;  // byte offsets into buf
+  std::shared_ptr<NetSlot> net;  // set when the pattern runs as a bit-sliced network
+  // reconstruct by syndromes: encode the received data (erased shards skipped) into
+  // a scratch, then the e x e matrix kernel on rec ^ scratch rows (see syndrome_map)
+  bool syndrome = false;
+  std::shared_ptr<DevBuf> skip;  // k-bit mask of the erased data shards
+  std::shared_ptr<FftSlot> syn_fft;  // the syndromes' encode on the bit-sliced FFT kernel (wide codes)
+  std::shared_ptr<FftSlot> inv_fft;  // every original lost, k == m == chunk: the encode inverted
+};
+
+// Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
+// kind) are dropped (a plan in use stays alive through its shared_ptr). g_plan_mu
+// guards the maps only: plans are built without it (double-checked insertion; two
+// threads racing on a new key may both build, the first insert wins).
+inline size_t plan_cache_cap() {
+  const char *e = std::getenv("RS_AMD_PLAN_CACHE");
+  return e && *e ? static_cast<size_t>(std::max(1, std::atoi(e))) : 4096u;
+}
+
+template <class V>
+struct PlanCache {
+  std::map<std::string, std::pair<std::shared_ptr<V>, uint64_t>> m;  // plan, last use
+  uint64_t tick = 0;
+  std::shared_ptr<V> find(const std::string &k) {  // g_plan_mu held
+    auto it = m.find(k);
+    if (it == m.end()) return nullptr;
+    it->second.second = ++tick;
+    return it->second.first;
+  }
+  std::shared_ptr<V> insert(const std::string &k, std::shared_ptr<V> v) {  // g_plan_mu held
+    auto it = m.find(k);
+    if (it != m.end()) {
+      it->second.second = ++tick;
+      return it->second.first;
+    }
+    const size_t cap = plan_cache_cap();
+    if (m.size() >= cap) {  // drop the oldest eighth (amortised O(1) per insert)
+      std::vector<std::pair<uint64_t, std::string>> age;
+      age.reserve(m.size());
+      for (auto &kv : m) age.emplace_back(kv.second.second, kv.first);
+      const size_t drop = std::max<size_t>(1, m.size() - cap + cap / 8);
+      std::nth_element(age.begin(), age.begin() + (drop - 1), age.end());
+      for (size_t i = 0; i < drop; i++) m.erase(age[i].second);
+    }
+    m.emplace(k, std::make_pair(v, ++tick));
+    return v;
+  }
+  size_t size() const { return m.size(); }
+};
+
+extern std::mutex g_plan_mu;
+int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out);
+
+constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
+
+// ------------------------------------------------- kernel selection (rs_select.cpp)
+bool encode_net_async(uint64_t k, uint64_t m);
+bool encode_net_ok(uint64_t sb);
+uint64_t fft_decode_mul_count(uint64_t k, uint64_t m, uint64_t present_count, uint64_t e);
+uint64_t fft_encode_mul_count(uint64_t k, uint64_t m);
+const char *decode_mode_env();
+constexpr uint32_t flags_none() { return 0; }
+int decode_kind(uint64_t k, uint64_t m, uint32_t flags, uint64_t e, uint64_t present_count, uint64_t sb);
+bool syndrome_pick(uint64_t k, uint64_t m, uint64_t e, uint32_t flags, uint64_t sb, const std::string &mode);
+bool direct_net_async(uint64_t e, uint64_t n_in, uint64_t sb, const std::string &mode, uint64_t k, uint64_t m,
+                      uint32_t flags);
+const char *net_name(const char *role, uint64_t n_in, uint64_t n_out);
+
+// ------------------------------------------------------------- plans (rs_plans.cpp)
+void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
+void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
+int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &ns);
+int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out);
+int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
+                    std::shared_ptr<DecodePlan> &out);
+
+// ---------------------------------------------------------- low rate (rs_lowrate.cpp)
+int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *orig, uint64_t ostride,
+               uint8_t *rec, uint64_t rstride, uint32_t flags, int max_nv, hipStream_t s);
+int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *present,
+                    const uint8_t *orig, uint64_t ostride, const uint8_t *rec, uint64_t rstride, uint8_t *out,
+                    uint64_t outstride, uint32_t flags, int max_nv, hipStream_t s);
+const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb);
+const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e);
+int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
+void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
+
+// -------------------------------------------------------- patterns (rs_patterns.cpp)
+// exp, log, log_walsh in HBM (384 KiB per device)
+int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw);
+
+}  // namespace host
+}  // namespace rs
