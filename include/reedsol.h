@@ -43,7 +43,7 @@ typedef enum rs_status {
   RS_ERR_TOO_MANY_SHARDS = 9,          /* root.zig:242, 258 */
   RS_ERR_OUT_OF_MEMORY = 10,           /* allocator failure */
   RS_ERR_OVERFLOW = 11,                /* std.math.ceilPowerOfTwo */
-  RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO") */
+  RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO"); here only per-stripe patterns */
   RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* root.zig:385 @panic("TODO"); here only rs_reconstruct_batch_dev_patterns */
   RS_ERR_INVALID_ARGUMENT = 14,        /* NULL pointer / bad stride */
   RS_ERR_DEVICE = 15,                  /* HIP runtime error (message: rs_last_error()) */
@@ -231,6 +231,14 @@ int rs_fft_compile_check(uint64_t original_count, uint64_t recovery_count, uint3
  * = wrong parity symbols over `trials` random stripes. */
 int rs_fft_selftest(uint64_t original_count, uint64_t recovery_count, uint32_t flags, const uint8_t *skip,
                     int trials, uint64_t *mismatches);
+
+/* Host check of the low-rate reconstruct's algebra (no device): `trials` random stripes
+ * of one symbol per shard, encoded by the low-rate encode, lose 1..min(k, m) random
+ * originals plus random recovery shards (>= k present), and are restored by the
+ * erasure-locator decode in the low-rate layout (rs_lowrate.cpp). *mismatches = wrong
+ * restored symbols. RS_ERR_INVALID_ARGUMENT for a high-rate code. */
+int rs_lowrate_selftest(uint64_t original_count, uint64_t recovery_count, int trials, uint64_t seed,
+                        uint64_t *mismatches);
 
 /* ---------------------------------------- Engine seam (Generic.zig), test shim
  * The reference's comptime Engine interface (root.zig:10-12) at per-call

@@ -53,18 +53,11 @@ int use_high_rate(uint64_t original, uint64_t recovery) {
   return original <= recovery ? 1 : 0;
 }
 
-// Low rate runs as maps of k x m GF(2^16) constants (passes of <= 64 outputs): the
-// map size bounds the tables (96 B per entry) and the reconstruct's 16e x 16e solve.
-constexpr uint64_t kLowRateMaxMap = 1ull << 16;
-inline bool low_rate_ok(uint64_t k, uint64_t m) { return k * m <= kLowRateMaxMap; }
-
 // Encoder.init / Decoder.init checks (root.zig:100-103, 198-201) + the tail panic (root.zig:385)
 int check_codec(uint64_t k, uint64_t m, size_t shard_bytes) {
   const int hr = use_high_rate(k, m);
   if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
-  // low rate: the reference panics (root.zig:120); here maps with k * m <= 65536 (§8 f4)
-  if (hr == 0 && !low_rate_ok(k, m))
-    return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "low-rate codec with original_count * recovery_count > 65536");
+  // low rate (hr == 0): the reference panics (root.zig:120, 227); here rs_lowrate.cpp (§8 f4)
   if (shard_bytes == 0 || (shard_bytes & 1)) return fail(RS_ERR_INVALID_SHARD_SIZE, "shard_bytes is 0 or odd");
   // shard_bytes % 64 != 0: the reference panics (root.zig:385); handled here with
   // the tail layout of root.zig:338-348 (tail_* below).
@@ -152,6 +145,32 @@ const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
 }
 
 std::mutex g_plan_mu;
+
+namespace {
+std::map<std::string, std::shared_ptr<DevBuf>> g_twiddle_plans;  // IFFT+FFT tables of size W, skew_delta 0
+}  // namespace
+
+int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft) {
+  const bool d1 = flags & RS_FLAG_QUIRK_D1;
+  off_fft = ifft_tab_count(W) * sizeof(RsTab);
+  const std::string key = std::to_string(dev) + "/" + std::to_string(W) + "/" + std::to_string(d1);
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto it = g_twiddle_plans.find(key);
+    if (it != g_twiddle_plans.end()) {
+      out = it->second;
+      return RS_OK;
+    }
+  }
+  std::vector<RsTab> tabs;  // built without the lock (65536-point tables take milliseconds)
+  push_ifft_tabs(tabs, W, 0, d1);
+  push_fft_tabs(tabs, W, 0, d1);
+  std::shared_ptr<DevBuf> buf;
+  if (int st = upload(tabs.data(), tabs.size() * sizeof(RsTab), dev, buf)) return st;
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_twiddle_plans.emplace(key, buf).first->second;  // first insert wins
+  return RS_OK;
+}
 
 int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out) {
   auto b = std::make_shared<DevBuf>();

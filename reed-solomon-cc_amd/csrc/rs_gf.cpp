@@ -239,6 +239,33 @@ void scalar_encode_low(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1
   }
 }
 
+void erasure_logs_low(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *er) {
+  const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end);
+  std::memset(er, 0, kOrder * sizeof(uint16_t));
+  for (uint64_t i = 0; i < k; i++)
+    if (!received[i]) er[i] = 1;  // missing originals; [k, C) are known zeros
+  for (uint64_t i = C; i < end; i++)
+    if (!received[i]) er[i] = 1;  // missing recovery
+  for (uint64_t i = end; i < W; i++) er[i] = 1;  // P's values past the code: unknown
+  eval_poly(er, W);
+}
+
+void scalar_reconstruct_low(uint16_t *sym, const uint8_t *received, const uint16_t *er, uint64_t k, uint64_t m) {
+  const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end);
+  for (uint64_t i = 0; i < W; i++) {
+    const bool live = (i < k || (i >= C && i < end)) && received[i];
+    sym[i] = live ? mul16(sym[i], er[i]) : 0;
+  }
+  scalar_ifft(sym, W, end, 0, false);
+  for (uint64_t i = 1; i < W; i++) {
+    const uint64_t w = i & (~i + 1);
+    for (uint64_t j = 0; j < w; j++) sym[i - w + j] ^= sym[i + j];
+  }
+  scalar_fft(sym, W, k, 0, false);
+  for (uint64_t i = 0; i < k; i++)
+    if (!received[i]) sym[i] = mul16(sym[i], static_cast<uint16_t>(kModulus - er[i]));
+}
+
 RsTab make_twiddle(uint32_t skew_index, bool quirk_d1) {
   if (skew_index >= kModulus) {  // beyond the table: only reachable for groups the device skips
     RsTab z{};

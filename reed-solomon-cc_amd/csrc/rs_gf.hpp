@@ -86,6 +86,16 @@ void scalar_encode(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, bo
 // [0, k) of a chunk C = ceilPow2(k): IFFT(size C, trunc k, skew 0); recovery
 // chunk j = FFT(copy, size C, trunc min(C, m - jC), skew (j+1)C).
 void scalar_encode_low(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1, uint16_t *out);
+// Low-rate reconstruct (the decode the low-rate encode above implies; parity unpinned).
+// The low-rate codeword is the evaluation of one polynomial P of degree < C on positions
+// [0, C + m): originals at [0, k), known zeros at [k, C) (the encode's zero padding), recovery
+// at [C, C + m). In a W = ceilPow2(C + m) point transform the positions [C + m, W) hold
+// unknown values of P, so they join the erasures (missing originals, missing recovery);
+// [k, C) stay received zeros. Then the formal-derivative decode of root.zig:268-335:
+// evalPoly(W) -> received x g^e -> IFFT(W, trunc C + m) -> derivative -> FFT(W, trunc k) ->
+// missing original i x g^(65535 - e_i). `received` has W entries in this position layout.
+void erasure_logs_low(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *out);
+void scalar_reconstruct_low(uint16_t *sym, const uint8_t *received, const uint16_t *erasures, uint64_t k, uint64_t m);
 // IFFT chunk truncations of the encode schedule (root.zig:143-166; D2 drops the last full chunk)
 std::vector<uint64_t> encode_chunk_truncs(uint64_t k, uint64_t m, bool quirk_d2);
 // root.zig:277-289: erasure flags for a received pattern -> evalPoly -> logs (65536 entries)

@@ -173,6 +173,9 @@ struct PlanCache {
 
 extern std::mutex g_plan_mu;
 int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out);
+// IFFT + FFT tables of size W at skew 0 (decode transforms), per (device, W, D1), in
+// HBM for the life of the process; *off_fft = byte offset of the FFT tables
+int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft);
 
 constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
 

@@ -55,7 +55,8 @@ struct DecodeArgs {
   const int32_t *pos_src;
   const int32_t *pos_dst;
   uint32_t work;   // W
-  uint32_t trunc;  // chunk + k
+  uint32_t trunc;  // chunk + k (IFFT truncation; the FFT's too unless trunc_fft is set)
+  uint32_t trunc_fft = 0;  // low rate: FFT truncated to k (only positions [0, k) are read)
   uint8_t *scratch;  // generic path only: [stripe][W][sb]
   uint64_t scratch_stripes;
   // matrix variant: restored[j] = XOR_i map_ij(in[i]) over n_in received shards
@@ -97,6 +98,15 @@ struct KernelChoice {
 // max_nv: widest per-lane access (1, 2, 4 dword pairs) the pointer/stride alignment allows
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
+KernelChoice choose_decode_w(uint64_t W, uint64_t shard_bytes, int max_nv);  // by transform size
+
+// Low-rate encode (rs_gf.hpp scalar_encode_low): EncodeArgs with chunk = C = ceilPow2(k),
+// k, m, n_chunks = recovery chunks ceil(m / C), tabs = ifft_tab_count(C) tables of
+// IFFT(C, skew 0) then tabs_per_chunk = fft_tab_count(C) tables of FFT(C, skew (j+1)C) per
+// recovery chunk j. Register kernel for C <= 32, else the scratch-walking generic kernel
+// (scratch [stripe][2C][sb]).
+KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv);
+hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
 // reconstruct as an n_out x n_in matrix of GF(2)-linear maps (decode matrix + GF MAC)
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv);
 constexpr uint32_t kMatrixMaxOut = 8;

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_reg(DecodeArgs a) {
     }
     dev::ifft_regs<W>(w, a.tab_ifft, a.trunc);  // root.zig:306
     derivative_regs<W>(w);                      // root.zig:309-315
-    dev::fft_regs<W>(w, a.tab_fft, a.trunc);    // root.zig:318
+    dev::fft_regs<W>(w, a.tab_fft, a.trunc_fft ? a.trunc_fft : a.trunc);  // root.zig:318
     uint8_t *out = a.out + s * a.out_stripe_stride;
 #pragma unroll
     for (int p = 0; p < W; p++) {  // root.zig:321-326
@@ -924,7 +924,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
       const uint64_t width = i & (~i + 1);
       for (uint64_t j = 0; j < width; j++) xor_mem<NV>(work + (i - width + j) * sb, work + (i + j) * sb);
     }
-    fft_mem<NV>(work, sb, 0, W, a.trunc, a.tab_fft);
+    fft_mem<NV>(work, sb, 0, W, a.trunc_fft ? a.trunc_fft : a.trunc, a.tab_fft);
     uint8_t *out = a.out + s * a.out_stripe_stride + off;
     for (uint64_t p = 0; p < W; p++) {
       const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
@@ -933,6 +933,88 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
         ld(v, work + p * sb);
         dev::mul_inplace(v, dev::load_tab(tab_post + p));
         dev::store_sym(out + static_cast<uint64_t>(dst) * sb, 0u, v, a.contig);
+      }
+    }
+  }
+}
+
+// ======================================================= low-rate encode (§8 f4)
+// The reference panics on low rate (root.zig:119-121); this is the encode of the
+// algorithm it ports (rs_gf.hpp scalar_encode_low, parity unpinned): the k originals are
+// positions [0, k) of one chunk C = ceilPow2(k), coefficients = IFFT(C, trunc k, skew 0),
+// and recovery chunk j = FFT(coefficients, trunc min(C, m - jC), skew (j+1)C).
+// Register kernel: the coefficients stay in VGPRs across the recovery chunks (each
+// chunk's FFT runs on a copy), so a stripe's originals are read once and every
+// recovery shard written once; twiddle tables are wave-uniform (SGPRs).
+template <int C, int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_low_reg(EncodeArgs a) {
+  uint32_t off;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
+  constexpr int TI = ifft_tabs_ce(C);
+  const uint64_t sb = a.shard_bytes;
+  const uint64_t s = blockIdx.y;  // launches are split at 65535 stripes
+  const uint8_t *src = a.data + s * a.data_stripe_stride;
+  Sym<NV> coef[C];
+#pragma unroll
+  for (int p = 0; p < C; p++) {
+    if (static_cast<uint32_t>(p) < a.k) dev::load_sym_raw(coef[p], src + p * sb, off, a.contig);
+    else dev::zero(coef[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < C; p++) dev::pair_halves(coef[p], a.contig);
+  dev::ifft_regs<C>(coef, a.tabs, a.k);
+  uint8_t *dst = a.parity + s * a.parity_stripe_stride;
+  for (uint32_t j = 0; j < a.n_chunks; j++) {
+    const uint32_t t = a.m - j * C < static_cast<uint32_t>(C) ? a.m - j * C : static_cast<uint32_t>(C);
+    Sym<NV> cur[C];
+#pragma unroll
+    for (int p = 0; p < C; p++) cur[p] = coef[p];
+    const RsTab *tj = a.tabs + TI + static_cast<uint64_t>(j) * a.tabs_per_chunk;
+    asm volatile("" : "+s"(tj));  // opaque base: no per-group pointer IVs
+    dev::fft_regs<C>(cur, tj, t);
+    uint8_t *dj = dst + static_cast<uint64_t>(j) * C * sb;
+#pragma unroll
+    for (int p = 0; p < C; p++)
+      if (static_cast<uint32_t>(p) < t) dev::store_sym(dj + p * sb, off, cur[p], a.contig);
+  }
+}
+
+// Any C: each lane walks its column through a scratch [stripe][2C][sb] (coefficients
+// at [0, C), the current recovery chunk at [C, 2C)).
+__device__ __forceinline__ uint64_t ifft_tab_count_d(uint64_t size) {
+  uint64_t n = 0, d = 1, d4 = 4;
+  for (; d4 <= size; d = d4, d4 <<= 2) n += 3 * (size / d4);
+  return n + (d < size ? 1 : 0);
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_low_generic(EncodeArgs a) {
+  uint32_t off;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
+  const uint64_t sb = a.shard_bytes, C = a.chunk, TI = ifft_tab_count_d(C);
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    const uint8_t *src = a.data + s * a.data_stripe_stride + off;
+    uint8_t *work = a.scratch + s * 2 * C * sb + off;
+    for (uint64_t p = 0; p < C; p++) {
+      Sym<NV> v;
+      if (p < a.k) ld(v, src + p * sb);
+      else dev::zero(v);
+      st(work + p * sb, v);
+    }
+    ifft_mem<NV>(work, sb, 0, C, a.k, a.tabs);
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride;
+    for (uint64_t j = 0; j < a.n_chunks; j++) {
+      const uint64_t t = a.m - j * C < C ? a.m - j * C : C;
+      for (uint64_t p = 0; p < C; p++) {
+        Sym<NV> v;
+        ld(v, work + p * sb);
+        st(work + (C + p) * sb, v);
+      }
+      fft_mem<NV>(work, sb, C, C, t, a.tabs + TI + j * a.tabs_per_chunk);
+      for (uint64_t p = 0; p < t; p++) {
+        Sym<NV> v;
+        ld(v, work + (C + p) * sb);
+        dev::store_sym(dst + (j * C + p) * sb, 0u, v, a.contig);
       }
     }
   }
@@ -1650,7 +1732,10 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
 }
 
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv) {
-  const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
+  return choose_decode_w(ceil_pow2(ceil_pow2(m) + k), shard_bytes, max_nv);
+}
+
+KernelChoice choose_decode_w(uint64_t W, uint64_t shard_bytes, int max_nv) {
   if (W <= 32) {
     const int w = static_cast<int>(W);
     const int nv = clamp_nv(fit_nv(std::min(env_nv(4), max_nv), shard_bytes), w, false);
@@ -1658,6 +1743,56 @@ KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
   }
   return {Variant::kGeneric, static_cast<int>(W), 1, "decode_generic_nv1"};
 }
+
+KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv) {
+  static const char *kNames[6][3] = {
+      {"encode_low_reg_w1_nv1", "encode_low_reg_w1_nv2", "encode_low_reg_w1_nv4"},
+      {"encode_low_reg_w2_nv1", "encode_low_reg_w2_nv2", "encode_low_reg_w2_nv4"},
+      {"encode_low_reg_w4_nv1", "encode_low_reg_w4_nv2", "encode_low_reg_w4_nv4"},
+      {"encode_low_reg_w8_nv1", "encode_low_reg_w8_nv2", "encode_low_reg_w8_nv4"},
+      {"encode_low_reg_w16_nv1", "encode_low_reg_w16_nv2", "encode_low_reg_w16_nv4"},
+      {"encode_low_reg_w32_nv1", "encode_low_reg_w32_nv2", "encode_low_reg_w32_nv4"}};
+  if (C <= 32) {  // coefficients + one recovery chunk live: the encode register budget
+    const int c = static_cast<int>(C);
+    const int nv = clamp_nv(fit_nv(std::min(env_nv(4), max_nv), shard_bytes), c, true);
+    int si = 0;
+    while ((1 << si) < c) si++;
+    return {Variant::kRegister, c, nv, kNames[si][nv == 1 ? 0 : nv == 2 ? 1 : 2]};
+  }
+  return {Variant::kGeneric, static_cast<int>(C), 1, "encode_low_generic_nv1"};
+}
+
+#define RS_ENC_LOW_CASE(C_, NV_)                                                  \
+  if (kc.size == C_ && kc.nv == NV_) {                                            \
+    hipLaunchKernelGGL((k_encode_low_reg<C_, NV_>), grid, dim3(kBlock), 0, s, b); \
+    e = hipGetLastError();                                                        \
+    if (e != hipSuccess) return e;                                                \
+    continue;                                                                     \
+  }
+
+hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
+  if (kc.variant == Variant::kGeneric) {
+    hipLaunchKernelGGL(k_encode_low_generic<1>, grid_for(a.shard_bytes, 1, a.n_stripes), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+  }
+  for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {
+    EncodeArgs b = a;
+    b.data += s0 * a.data_stripe_stride;
+    b.parity += s0 * a.parity_stripe_stride;
+    b.n_stripes = std::min<uint64_t>(65535, a.n_stripes - s0);
+    const dim3 grid = grid_for(b.shard_bytes, kc.nv, b.n_stripes);
+    hipError_t e = hipSuccess;
+    RS_ENC_LOW_CASE(1, 1) RS_ENC_LOW_CASE(1, 2) RS_ENC_LOW_CASE(1, 4)
+    RS_ENC_LOW_CASE(2, 1) RS_ENC_LOW_CASE(2, 2) RS_ENC_LOW_CASE(2, 4)
+    RS_ENC_LOW_CASE(4, 1) RS_ENC_LOW_CASE(4, 2) RS_ENC_LOW_CASE(4, 4)
+    RS_ENC_LOW_CASE(8, 1) RS_ENC_LOW_CASE(8, 2)
+    RS_ENC_LOW_CASE(16, 1)
+    RS_ENC_LOW_CASE(32, 1)
+    return hipErrorInvalidValue;
+  }
+  return hipSuccess;
+}
+#undef RS_ENC_LOW_CASE
 
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv) {
   static const char *kNames[9][3] = {

@@ -1,18 +1,56 @@
-// rs_lowrate.cpp — the low-rate codec (§8 f4; the reference panics: root.zig:119-121, 226-228).
+// rs_lowrate.cpp — the low-rate codec (§8 f4): pow2(k) < pow2(m), or equal with k > m.
+//
+// The reference panics here (root.zig:119-121, 226-228) and vendors no low-rate code, so
+// this is the low-rate codec of the algorithm it ports (reed-solomon-simd, named in
+// benchmarks.zig:1-2): PARITY UNPINNED, no reference output exists. Quirk flags are
+// ignored (D1 / D2 are defects of the reference's high-rate path; there is no literal
+// low-rate behaviour to reproduce): the corrected multiply always.
+//
+//  * encode (rs_gf.hpp scalar_encode_low): originals at positions [0, k) of one chunk
+//    C = ceilPow2(k), coefficients = IFFT(C, trunc k, skew 0), recovery chunk j =
+//    FFT(coefficients, trunc min(C, m - jC), skew (j + 1) C). FFT-form kernels
+//    (rs_kernels.hip k_encode_low_reg for C <= 32, k_encode_low_generic otherwise).
+//  * reconstruct (rs_gf.hpp scalar_reconstruct_low): the erasure-locator decode of
+//    root.zig:268-335 in the low-rate position layout (recovery at [C, C + m), [C + m, W)
+//    erased), on the decode kernels with the FFT truncated to k (k_decode_reg for
+//    W <= 32, k_decode_generic otherwise) — no host solve, any (k, m) useHighRate accepts.
+//  * small codes: a bit-sliced network of the encode map (<= 64 outputs) and of each
+//    erasure pattern's reconstruct map (<= 64 restored, by GF(2) linear algebra on the
+//    host), HBM-bound; the FFT-form kernels run until such a network is compiled.
 #include "rs_host.hpp"
 
 namespace rs {
 namespace host {
 
-// ------------------------------------------------------- low-rate codec (§8 f4)
-// The reference panics on low rate (root.zig:119-121, 226-228). Here the encode
-// is reed-solomon-simd's low-rate encoder (rs_gf.hpp scalar_encode_low; parity
-// unpinned: no reference output exists) and a reconstruct is the unique MDS
-// solution, derived by linear algebra from the encode map. Both run as maps on
-// the network kernels, or on the table matrix kernels in groups of <= 8 outputs.
+namespace {
+
+// single-pass maps only (every output of the map in one network kernel)
+bool map_net_ok(uint64_t n_in, uint64_t n_out, uint64_t sb) {
+  return jit::enabled() && n_out > 0 && n_out <= jit::kMaxOut &&
+         jit::supports_async(static_cast<uint32_t>(n_in), static_cast<uint32_t>(n_out), sb);
+}
+
+struct LowEncodePlan {
+  std::shared_ptr<DevBuf> tabs;  // IFFT(C, skew 0), then FFT(C, skew (j+1)C) per recovery chunk
+  uint32_t C = 0, n_chunks = 0, tabs_per_chunk = 0;
+  std::shared_ptr<NetSlot> net;  // the encode map's network (small codes)
+};
+
+struct LowDecodePlan {
+  std::shared_ptr<DevBuf> tw;    // IFFT + FFT tables of size W (shared per W)
+  std::shared_ptr<DevBuf> buf;   // pre[W] | post[W] RsTab, src[W] | dst[W] int32
+  size_t off_fft = 0;
+  uint32_t W = 0, trunc = 0, e = 0;
+  std::shared_ptr<NetSlot> net;  // the pattern's reconstruct map (small codes)
+};
+
+PlanCache<LowEncodePlan> g_low_enc;
+PlanCache<LowDecodePlan> g_low_dec;  // a W = 65536 plan holds 13 MB of HBM: plans are LRU-capped
+
+}  // namespace
 
 void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
-  const bool d1 = flags & RS_FLAG_QUIRK_D1;
+  (void)flags;  // corrected multiply (quirks have no low-rate meaning)
   ns.role = "encode_low";
   ns.n_in = static_cast<uint32_t>(k);
   ns.n_out = static_cast<uint32_t>(m);
@@ -23,13 +61,14 @@ void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
     ns.src.push_back(static_cast<int32_t>(t));
     for (int b = 0; b < 16; b++) {
       in[t] = static_cast<uint16_t>(1u << b);
-      scalar_encode_low(in.data(), k, m, d1, out.data());
+      scalar_encode_low(in.data(), k, m, false, out.data());
       for (uint64_t j = 0; j < m; j++) ns.images[(t * m + j) * 16 + b] = out[j];
     }
     in[t] = 0;
   }
 }
 
+namespace {
 // Reconstruct of a systematic linear code with encode map G (G.images[(t*m + r)*16 + b]
 // = parity r of basis b at data t): with E the erased data, P the present data and R
 // the first e present recovery rows, p_R = G_RE x + G_RP d_P, so
@@ -84,130 +123,7 @@ int linear_decode_map(uint64_t k, uint64_t m, const jit::NetSpec &G, const uint8
   return RS_OK;
 }
 
-// A map on the device, in passes of <= 64 outputs (jit::kMaxOut; every pass reads
-// all inputs): per pass the network kernel when it fits, else the table matrix
-// kernels over groups of <= 8 outputs (blocks [group][n_in][E_g] of tables + src).
-struct MapPlan {
-  std::shared_ptr<DevBuf> buf;
-  uint32_t n_in = 0, n_out = 0;
-  std::vector<size_t> group_off;  // byte offset of each group's table block
-  size_t off_src = 0;
-  std::vector<std::shared_ptr<NetSlot>> net;  // per pass: outputs [64 p, 64 p + 64)
-};
-
-inline uint32_t map_passes(uint32_t n_out) { return (n_out + jit::kMaxOut - 1) / jit::kMaxOut; }
-// every pass of an n_in x n_out map has a network form (the first pass is the widest)
-bool map_net_ok(uint64_t n_in, uint64_t n_out, uint64_t sb) {
-  return jit::enabled() && n_out > 0 &&
-         jit::supports_async(static_cast<uint32_t>(n_in), static_cast<uint32_t>(std::min<uint64_t>(n_out, jit::kMaxOut)), sb);
-}
-PlanCache<MapPlan> g_map_plans;
-
-int build_map_plan(int dev, jit::NetSpec &&spec, std::shared_ptr<MapPlan> &out) {
-  auto p = std::make_shared<MapPlan>();
-  p->n_in = spec.n_in;
-  p->n_out = spec.n_out;
-  std::vector<RsTab> tabs;
-  for (uint32_t j0 = 0; j0 < spec.n_out; j0 += kMatrixMaxOut) {
-    const uint32_t eg = std::min<uint32_t>(kMatrixMaxOut, spec.n_out - j0);
-    p->group_off.push_back(tabs.size() * sizeof(RsTab));
-    for (uint32_t t = 0; t < spec.n_in; t++)
-      for (uint32_t j = 0; j < eg; j++)
-        tabs.push_back(make_tab_from_images(&spec.images[(static_cast<size_t>(t) * spec.n_out + j0 + j) * 16]));
-  }
-  std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + spec.n_in * sizeof(int32_t));
-  std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
-  std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), spec.src.data(), spec.n_in * sizeof(int32_t));
-  p->off_src = tabs.size() * sizeof(RsTab);
-  int st = upload(blob.data(), blob.size(), dev, p->buf);
-  if (st) return st;
-  for (uint32_t j0 = 0; j0 < spec.n_out; j0 += jit::kMaxOut) {
-    const uint32_t len = std::min<uint32_t>(jit::kMaxOut, spec.n_out - j0);
-    auto slot = std::make_shared<NetSlot>();
-    slot->async = !jit::supports(p->n_in, len, jit::kUnitBytes);  // larger maps: background compile
-    jit::NetSpec &ps = slot->spec;
-    ps.role = spec.role;
-    ps.n_in = spec.n_in;
-    ps.n_out = len;
-    ps.src = spec.src;
-    if (len == spec.n_out) {
-      ps.images = std::move(spec.images);
-    } else {
-      ps.images.resize(static_cast<size_t>(spec.n_in) * len * 16);
-      for (uint32_t t = 0; t < spec.n_in; t++)
-        std::memcpy(&ps.images[static_cast<size_t>(t) * len * 16],
-                    &spec.images[(static_cast<size_t>(t) * spec.n_out + j0) * 16], len * 16 * sizeof(uint16_t));
-    }
-    p->net.push_back(std::move(slot));
-  }
-  out = p;
-  return RS_OK;
-}
-
-int run_map_pass(const MapPlan &p, uint32_t pi, bool net_ok, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0,
-                 const uint8_t *b1, uint64_t s1, uint8_t *out, uint64_t so, int max_nv, hipStream_t s);
-
-// out[j] = sum_i map_ij(in_i) for every stripe; inputs per src (buffer 0 / 1).
-int run_map(const MapPlan &p, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0, const uint8_t *b1, uint64_t s1,
-            uint8_t *out, uint64_t so, int max_nv, hipStream_t s) {
-  if (!b0) b0 = b1;
-  if (!b1) b1 = b0;
-  const bool net_ok = max_nv == 4 && map_net_ok(p.n_in, p.n_out, sb);
-  for (uint32_t pi = 0; pi < p.net.size(); pi++)
-    if (int st = run_map_pass(p, pi, net_ok, sb, n, b0, s0, b1, s1, out, so, max_nv, s)) return st;
-  return RS_OK;
-}
-
-int run_map_pass(const MapPlan &p, uint32_t pi, bool net_ok, uint64_t sb, uint64_t n, const uint8_t *b0, uint64_t s0,
-                 const uint8_t *b1, uint64_t s1, uint8_t *out, uint64_t so, int max_nv, hipStream_t s) {
-  const uint32_t p0 = pi * jit::kMaxOut, p1 = std::min<uint32_t>(p.n_out, p0 + jit::kMaxOut);
-  if (net_ok)
-    if (const jit::Kernel *nk = net_kernel(*p.net[pi], sb)) {
-      HIP_TRY(jit::launch(*nk, b0, s0, b1, s1, out + static_cast<uint64_t>(p0) * sb, so, sb, n, s));
-      return RS_OK;
-    }
-  const uint8_t *base = static_cast<const uint8_t *>(p.buf->p);
-  for (size_t g = p0 / kMatrixMaxOut; g < p.group_off.size() && g * kMatrixMaxOut < p1; g++) {
-    const uint32_t j0 = static_cast<uint32_t>(g * kMatrixMaxOut);
-    const uint32_t eg = std::min<uint32_t>(kMatrixMaxOut, p.n_out - j0);
-    const KernelChoice kc = choose_decode_matrix(eg, sb, max_nv);
-    DecodeArgs a{};
-    a.orig = b0;
-    a.orig_stripe_stride = s0;
-    a.rec = b1;
-    a.rec_stripe_stride = s1;
-    a.out = out + static_cast<uint64_t>(j0) * sb;
-    a.out_stripe_stride = so;
-    a.shard_bytes = sb;
-    a.tab_mat = reinterpret_cast<const RsTab *>(base + p.group_off[g]);
-    a.pos_src = reinterpret_cast<const int32_t *>(base + p.off_src);
-    a.n_in = p.n_in;
-    a.n_out = eg;
-    a.contig = contig_ok(sb, kc.nv);
-    a.n_stripes = n;
-    // launch_decode advances these per 65535-stripe slice: keep them valid
-    a.tab_pre = a.tab_post = a.tab_mat;
-    a.pos_dst = a.pos_src;
-    HIP_TRY(launch_decode(kc, a, s));
-  }
-  return RS_OK;
-}
-
-int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<MapPlan> &out) {
-  const std::string key = "lowenc/" + std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                          std::to_string(flags & RS_FLAG_QUIRK_D1);
-  {
-    std::lock_guard<std::mutex> lk(g_plan_mu);
-    if ((out = g_map_plans.find(key))) return RS_OK;
-  }
-  jit::NetSpec spec;
-  encode_low_map(k, m, flags, spec);
-  int st = build_map_plan(dev, std::move(spec), out);
-  if (st) return st;
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  out = g_map_plans.insert(key, out);
-  return RS_OK;
-}
+}  // namespace
 
 int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns) {
   jit::NetSpec G;
@@ -215,45 +131,203 @@ int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *presen
   return linear_decode_map(k, m, G, present, "reconstruct_low", ns);
 }
 
-int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present,
-                        std::shared_ptr<MapPlan> &out) {
-  std::string key = "lowdec/" + std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                    std::to_string(flags & RS_FLAG_QUIRK_D1) + "/";
-  for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
+namespace {
+
+int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, std::shared_ptr<LowEncodePlan> &out) {
+  const bool net = map_net_ok(k, m, sb);
+  const std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                          std::to_string(net) + "/" + std::to_string(jit::max_blocks());
   {
     std::lock_guard<std::mutex> lk(g_plan_mu);
-    if ((out = g_map_plans.find(key))) return RS_OK;
+    if ((out = g_low_enc.find(key))) return RS_OK;
   }
-  jit::NetSpec spec;
-  int st = low_decode_map(k, m, flags, present, spec);
-  if (st) return st;
-  if ((st = build_map_plan(dev, std::move(spec), out))) return st;
+  auto p = std::make_shared<LowEncodePlan>();
+  const uint64_t C = ceil_pow2(k);
+  p->C = static_cast<uint32_t>(C);
+  p->n_chunks = static_cast<uint32_t>((m + C - 1) / C);
+  p->tabs_per_chunk = static_cast<uint32_t>(fft_tab_count(C));
+  std::vector<RsTab> tabs;
+  push_ifft_tabs(tabs, C, 0, false);
+  for (uint64_t j = 0; j < p->n_chunks; j++) push_fft_tabs(tabs, C, (j + 1) * C, false);
+  if (int st = upload(tabs.data(), std::max<size_t>(1, tabs.size()) * sizeof(RsTab), dev, p->tabs)) return st;
+  if (net) {
+    p->net = std::make_shared<NetSlot>();
+    p->net->async = !jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb);
+    encode_low_map(k, m, 0, p->net->spec);
+  }
   std::lock_guard<std::mutex> lk(g_plan_mu);
-  out = g_map_plans.insert(key, out);
+  out = g_low_enc.insert(key, p);
   return RS_OK;
 }
 
+int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present,
+                        std::shared_ptr<LowDecodePlan> &out) {
+  uint64_t e = 0;
+  for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+  const bool net = map_net_ok(k, e, sb);
+  std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                    std::to_string(net) + "/" + std::to_string(jit::max_blocks()) + "/";
+  key.reserve(key.size() + k + m);
+  for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if ((out = g_low_dec.find(key))) return RS_OK;
+  }
+  auto p = std::make_shared<LowDecodePlan>();
+  const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end);
+  p->W = static_cast<uint32_t>(W);
+  p->trunc = static_cast<uint32_t>(end);
+  if (int st = twiddle_plan(dev, W, 0, p->tw, p->off_fft)) return st;
+  // position layout of scalar_reconstruct_low: originals [0, k), recovery [C, C + m)
+  std::vector<uint8_t> received(W, 0);
+  for (uint64_t i = 0; i < k; i++) received[i] = present[i] ? 1 : 0;
+  for (uint64_t r = 0; r < m; r++) received[C + r] = present[k + r] ? 1 : 0;
+  std::vector<uint16_t> er(kOrder);
+  erasure_logs_low(received.data(), k, m, er.data());
+  std::vector<RsTab> tabs(2 * W);  // pre, post
+  std::vector<int32_t> idx(2 * W, -1);  // src, dst
+  uint32_t ne = 0;
+  for (uint64_t q = 0; q < W; q++) {
+    if (q < k && received[q]) {
+      idx[q] = static_cast<int32_t>(q);
+      tabs[q] = make_tab(er[q], false);
+    } else if (q >= C && q < end && received[q]) {
+      idx[q] = kSrcRecovery | static_cast<int32_t>(q - C);
+      tabs[q] = make_tab(er[q], false);
+    }
+    if (q < k && !received[q]) {
+      idx[W + q] = static_cast<int32_t>(ne++);
+      tabs[W + q] = make_tab(static_cast<uint16_t>(kModulus - er[q]), false);
+    }
+  }
+  p->e = ne;
+  std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + idx.size() * sizeof(int32_t));
+  std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
+  std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), idx.data(), idx.size() * sizeof(int32_t));
+  if (int st = upload(blob.data(), blob.size(), dev, p->buf)) return st;
+  if (net) {
+    p->net = std::make_shared<NetSlot>();
+    p->net->async = !jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb);
+    if (int st = low_decode_map(k, m, 0, present, p->net->spec)) return st;
+  }
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  out = g_low_dec.insert(key, p);
+  return RS_OK;
+}
+
+// generic kernels walk a scratch of `per_stripe` positions x sb per stripe, in slices
+template <class F>
+int in_scratch_slices(uint64_t n, uint64_t per_stripe_bytes, hipStream_t s, F &&launch) {
+  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n, kScratchCap / per_stripe_bytes));
+  void *scratch = nullptr;
+  HIP_TRY(hipMallocAsync(&scratch, per * per_stripe_bytes, s));
+  hipError_t e = hipSuccess;
+  for (uint64_t s0 = 0; e == hipSuccess && s0 < n; s0 += per)
+    e = launch(s0, std::min(per, n - s0), static_cast<uint8_t *>(scratch));
+  (void)hipFreeAsync(scratch, s);
+  return e == hipSuccess ? RS_OK : hip_fail(e, "low-rate generic kernel");
+}
+
+}  // namespace
+
 int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *orig, uint64_t ostride,
                uint8_t *rec, uint64_t rstride, uint32_t flags, int max_nv, hipStream_t s) {
-  std::shared_ptr<MapPlan> lp;
-  if (int st = get_low_encode_plan(dev, k, m, flags, lp)) return st;
-  return run_map(*lp, sb, n, orig, ostride, nullptr, 0, rec, rstride, max_nv, s);
+  (void)flags;
+  std::shared_ptr<LowEncodePlan> p;
+  if (int st = get_low_encode_plan(dev, k, m, sb, p)) return st;
+  if (p->net && max_nv == 4)
+    if (const jit::Kernel *nk = net_kernel(*p->net, sb)) {
+      HIP_TRY(jit::launch(*nk, orig, ostride, nullptr, 0, rec, rstride, sb, n, s));
+      return RS_OK;
+    }
+  const KernelChoice kc = choose_encode_low(p->C, sb, max_nv);
+  EncodeArgs a{};
+  a.data = orig;
+  a.data_stripe_stride = ostride;
+  a.parity = rec;
+  a.parity_stripe_stride = rstride;
+  a.shard_bytes = sb;
+  a.tabs = static_cast<const RsTab *>(p->tabs->p);
+  a.chunk = p->C;
+  a.n_chunks = p->n_chunks;
+  a.tabs_per_chunk = p->tabs_per_chunk;
+  a.k = static_cast<uint32_t>(k);
+  a.m = static_cast<uint32_t>(m);
+  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
+  if (kc.variant != Variant::kGeneric) {
+    a.n_stripes = n;
+    HIP_TRY(launch_encode_low(kc, a, s));
+    return RS_OK;
+  }
+  return in_scratch_slices(n, 2ull * p->C * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
+    EncodeArgs b = a;
+    b.data += s0 * ostride;
+    b.parity += s0 * rstride;
+    b.n_stripes = cnt;
+    b.scratch = scratch;
+    return launch_encode_low(kc, b, s);
+  });
 }
 
 int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *present,
                     const uint8_t *orig, uint64_t ostride, const uint8_t *rec, uint64_t rstride, uint8_t *out,
                     uint64_t outstride, uint32_t flags, int max_nv, hipStream_t s) {
-  std::shared_ptr<MapPlan> lp;
-  if (int st = get_low_decode_plan(dev, k, m, flags, present, lp)) return st;
-  return run_map(*lp, sb, n, orig, ostride, rec, rstride, out, outstride, max_nv, s);
+  (void)flags;
+  std::shared_ptr<LowDecodePlan> p;
+  if (int st = get_low_decode_plan(dev, k, m, sb, present, p)) return st;
+  if (!orig) orig = rec;  // never dereferenced for absent shards
+  if (!rec) rec = orig;
+  if (p->net && max_nv == 4)
+    if (const jit::Kernel *nk = net_kernel(*p->net, sb)) {
+      HIP_TRY(jit::launch(*nk, orig, ostride, rec, rstride, out, outstride, sb, n, s));
+      return RS_OK;
+    }
+  const KernelChoice kc = choose_decode_w(p->W, sb, max_nv);
+  const uint8_t *base = static_cast<const uint8_t *>(p->buf->p);
+  const uint8_t *tw = static_cast<const uint8_t *>(p->tw->p);
+  DecodeArgs a{};
+  a.orig = orig;
+  a.orig_stripe_stride = ostride;
+  a.rec = rec;
+  a.rec_stripe_stride = rstride;
+  a.out = out;
+  a.out_stripe_stride = outstride;
+  a.shard_bytes = sb;
+  a.tab_ifft = reinterpret_cast<const RsTab *>(tw);
+  a.tab_fft = reinterpret_cast<const RsTab *>(tw + p->off_fft);
+  a.tab_pre = reinterpret_cast<const RsTab *>(base);
+  a.tab_post = a.tab_pre + p->W;
+  a.pos_src = reinterpret_cast<const int32_t *>(base + 2ull * p->W * sizeof(RsTab));
+  a.pos_dst = a.pos_src + p->W;
+  a.work = p->W;
+  a.trunc = p->trunc;
+  a.trunc_fft = static_cast<uint32_t>(k);
+  a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
+  if (kc.variant != Variant::kGeneric) {
+    a.n_stripes = n;
+    HIP_TRY(launch_decode(kc, a, s));
+    return RS_OK;
+  }
+  return in_scratch_slices(n, static_cast<uint64_t>(p->W) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
+    DecodeArgs b = a;
+    b.orig += s0 * ostride;
+    b.rec += s0 * rstride;
+    b.out += s0 * outstride;
+    b.n_stripes = cnt;
+    b.scratch = scratch;
+    b.scratch_stripes = cnt;
+    return launch_decode(kc, b, s);
+  });
 }
 
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb) {
-  return map_net_ok(k, m, sb) ? net_name("encode_low", k, m) : "lowrate_matrix";
+  if (map_net_ok(k, m, sb)) return net_name("encode_low", k, m);
+  return choose_encode_low(ceil_pow2(k), sb, 4).name;
 }
 
 const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e) {
-  return map_net_ok(k, e, sb) ? net_name("reconstruct_low", k, e) : "lowrate_matrix";
+  if (map_net_ok(k, e, sb)) return net_name("reconstruct_low", k, e);
+  return choose_decode_w(ceil_pow2(ceil_pow2(k) + m), sb, 4).name;
 }
 
 }  // namespace host
@@ -262,3 +336,49 @@ const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uin
 using namespace rs;
 using namespace rs::host;
 
+extern "C" int rs_lowrate_selftest(uint64_t k, uint64_t m, int trials, uint64_t seed, uint64_t *mismatches) {
+  return guarded([&]() -> int {
+    const int hr = use_high_rate(k, m);
+    if (hr < 0) return fail(-hr, "unsupported shard count (root.zig:397-415)");
+    if (hr == 1) return fail(RS_ERR_INVALID_ARGUMENT, "not a low-rate code");
+    const uint64_t C = ceil_pow2(k), W = ceil_pow2(C + m);
+    uint64_t state = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() {  // splitmix64
+      uint64_t z = (state += 0x9E3779B97F4A7C15ull);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return z ^ (z >> 31);
+    };
+    uint64_t bad = 0;
+    std::vector<uint16_t> data(k), par(m), sym(W), er(kOrder);
+    std::vector<uint8_t> present(k + m), received(W);
+    for (int t = 0; t < trials; t++) {
+      for (auto &x : data) x = static_cast<uint16_t>(rnd());
+      scalar_encode_low(data.data(), k, m, false, par.data());
+      // lose e random originals (1..min(k, m)) and as many recovery shards as leaves >= k present
+      const uint64_t e = 1 + rnd() % std::min(k, m);
+      std::fill(present.begin(), present.end(), 1);
+      for (uint64_t c = 0; c < e;) {
+        const uint64_t i = rnd() % k;
+        if (present[i]) present[i] = 0, c++;
+      }
+      const uint64_t drop = rnd() % (m - e + 1);
+      for (uint64_t c = 0; c < drop;) {
+        const uint64_t r = rnd() % m;
+        if (present[k + r]) present[k + r] = 0, c++;
+      }
+      std::fill(received.begin(), received.end(), 0);
+      std::fill(sym.begin(), sym.end(), 0);
+      for (uint64_t i = 0; i < k; i++)
+        if (present[i]) received[i] = 1, sym[i] = data[i];
+      for (uint64_t r = 0; r < m; r++)
+        if (present[k + r]) received[C + r] = 1, sym[C + r] = par[r];
+      erasure_logs_low(received.data(), k, m, er.data());
+      scalar_reconstruct_low(sym.data(), received.data(), er.data(), k, m);
+      for (uint64_t i = 0; i < k; i++)
+        if (!present[i] && sym[i] != data[i]) bad++;
+    }
+    if (mismatches) *mismatches = bad;
+    return RS_OK;
+  });
+}

@@ -37,27 +37,6 @@ int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uin
 }  // namespace rs
 
 namespace {
-std::map<std::string, std::shared_ptr<DevBuf>> g_twiddle_plans;  // IFFT+FFT tables of size W, skew_delta 0
-
-int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft) {
-  const bool d1 = flags & RS_FLAG_QUIRK_D1;
-  std::vector<RsTab> tabs;
-  push_ifft_tabs(tabs, W, 0, d1);
-  off_fft = tabs.size() * sizeof(RsTab);
-  const std::string key = std::to_string(dev) + "/" + std::to_string(W) + "/" + std::to_string(d1);
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto it = g_twiddle_plans.find(key);
-  if (it != g_twiddle_plans.end()) {
-    out = it->second;
-    return RS_OK;
-  }
-  push_fft_tabs(tabs, W, 0, d1);
-  int st = upload(tabs.data(), tabs.size() * sizeof(RsTab), dev, out);
-  if (st) return st;
-  g_twiddle_plans.emplace(key, out);
-  return RS_OK;
-}
-
 // Per code (k, m, flags): the syndrome-network kernel of rs_psyn.hpp and the code's
 // encode coefficients G [m][k] in HBM (for the per-stripe plans).
 struct PsynPlan {

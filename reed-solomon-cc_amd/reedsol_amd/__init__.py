@@ -93,6 +93,7 @@ def lib():
         "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
         "rs_patterns_kernel_name": (C.c_char_p, [u64, u64, sz, u32, u32]),
         "rs_fft_selftest": (C.c_int, [u64, u64, u32, vp, C.c_int, vp]),
+        "rs_lowrate_selftest": (C.c_int, [u64, u64, C.c_int, u64, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_mul_scalar": (C.c_int, [vp, sz, C.c_uint16, u32]),
@@ -371,6 +372,13 @@ def psyn_compile_check(k, m, flags=0) -> dict:
     ms, b = C.c_double(), C.c_uint64()
     _check(lib().rs_psyn_compile_check(k, m, flags, C.byref(ms), C.byref(b)))
     return {"compile_ms": ms.value, "code_bytes": b.value}
+
+
+def lowrate_selftest(k, m, trials=8, seed=1) -> int:
+    """Host check of the low-rate reconstruct's algebra: wrong restored symbols."""
+    bad = C.c_uint64()
+    _check(lib().rs_lowrate_selftest(k, m, trials, seed, C.byref(bad)))
+    return bad.value
 
 
 def fft_selftest(k, m, flags=0, skip=None, trials=8) -> int:

@@ -70,8 +70,7 @@ def test_validation_precedes_device():
         R.Encoder(10, 4, 63)
     with pytest.raises(R.InvalidShardSize):
         R.Encoder(10, 4, 0)
-    with pytest.raises(R.LowRateUnsupported):
-        R.Encoder(200, 400, 64)  # low-rate map past k * m = 65536 (the reference panics on any low rate)
+    R.Encoder(200, 400, 64).deinit()  # low rate: accepted (the reference panics on any low rate)
     R.Encoder(10, 4, 66).deinit()  # tails accepted (root.zig:338-348 layout; the reference panics)
     with pytest.raises(R.TooFewOriginalShards):
         R.encode(10, 4, [])

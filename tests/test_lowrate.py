@@ -7,7 +7,8 @@ oracle (rso_encode_low) and in the library (rs_gf.cpp scalar_encode_low); the
 GPU encode is checked against that restatement, and reconstruct — unique for an
 MDS code — by round trips. The CPU tests pin the restatement's MDS property:
 every k-subset of a codeword determines the data (GF(2) rank of the 16k x 16k
-generator block)."""
+generator block), and the erasure-locator decode's algebra in the low-rate layout
+(rs_lowrate_selftest) for every size class up to 65,536-point transforms."""
 import itertools
 
 import numpy as np
@@ -16,8 +17,12 @@ import pytest
 from rs_amd import reedsol_amd as R
 
 LOW_KM = [(1, 2), (2, 4), (3, 5), (3, 6), (5, 9), (4, 16), (10, 20), (7, 40), (16, 64)]
-# past 64 recovery shards: maps in passes of <= 64 outputs (rs_capi.cpp MapPlan)
-LOW_KM_WIDE = [(2, 100), (10, 200), (3, 1000), (17, 130), (100, 600)]
+# past 64 recovery shards: FFT-form kernels (rs_lowrate.cpp), register (C <= 32) or generic
+LOW_KM_WIDE = [(2, 100), (10, 200), (3, 1000), (17, 130), (100, 600), (40, 100)]
+# the verdict's shapes past the old k * m <= 65536 map limit, and size-class extremes
+LOW_KM_LARGE = [(300, 1000), (200, 1000), (1000, 4000)]
+SELFTEST_KM = LOW_KM + LOW_KM_WIDE + LOW_KM_LARGE + [
+    (1, 65535), (2, 65534), (64, 65472), (16384, 40000), (30000, 20000), (32, 33), (60, 40), (33, 65), (255, 257)]
 
 
 def gf2_rank(rows):
@@ -73,20 +78,34 @@ def test_low_rate_network_compiles(k, m):
     assert R.net_compile_check(k, m) > 0
 
 
+@pytest.mark.parametrize("k,m", SELFTEST_KM)
+def test_low_rate_decode_algebra(k, m):
+    """scalar_reconstruct_low restores every lost original (host, one symbol per shard)."""
+    assert R.use_high_rate(k, m) is False
+    assert R.lowrate_selftest(k, m, trials=4, seed=k * 7 + m) == 0
+
+
 def test_low_rate_limits(monkeypatch):
     R.Encoder(2, 100, 64)
     R.Encoder(100, 600, 64)
-    with pytest.raises(R.LowRateUnsupported):  # k * m > 65536
-        R.Encoder(200, 400, 64)
-    with pytest.raises(R.LowRateUnsupported):
-        R.Encoder(16, 4097, 64)
-    assert R.encode_kernel_name(2, 100, 1 << 16) == "net_encode_low_i2_o100"
-    assert R.encode_kernel_name(100, 600, 1 << 16) == "lowrate_matrix"  # 100 x 64 per pass: past the network cap
+    R.Encoder(200, 400, 64)  # past the round-2 map limit k * m <= 65536
+    R.Encoder(16, 4097, 64)
+    R.Encoder(30000, 20000, 64)
+    with pytest.raises(R.UnsupportedShardCount):  # pow2(min) + max > 65536 (root.zig:407)
+        R.Encoder(32769, 40000, 64)
+    assert R.encode_kernel_name(2, 60, 1 << 16) == "net_encode_low_i2_o60"
+    assert R.encode_kernel_name(2, 100, 1 << 16) == "encode_low_reg_w2_nv4"  # > 64 outputs: FFT form
+    assert R.encode_kernel_name(100, 600, 1 << 16) == "encode_low_generic_nv1"
     assert R.encode_kernel_name(10, 20, 1 << 16) == "net_encode_low_i10_o20"
-    # 256 blocks: a background-compiled network (table matrix kernel until it is ready)
+    # 256 blocks: a background-compiled network (the FFT-form kernel until it is ready)
     assert R.encode_kernel_name(16, 64, 1 << 16) == "net_encode_low_i16_o64"
+    assert R.reconstruct_kernel_name(1000, 4000, 4096, [0] * 10 + [1] * 4990) == "decode_generic_nv1"
+    assert R.reconstruct_kernel_name(3, 5, 4096, [0, 1, 1] + [1] * 5).startswith("net_reconstruct_low")
     monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
-    assert R.encode_kernel_name(16, 64, 1 << 16) == "lowrate_matrix"
+    assert R.encode_kernel_name(16, 64, 1 << 16) == "encode_low_reg_w16_nv1"
+    monkeypatch.setenv("RS_AMD_JIT", "0")
+    assert R.encode_kernel_name(10, 20, 1 << 16) == "encode_low_reg_w16_nv1"
+    assert R.reconstruct_kernel_name(3, 5, 4096, [0, 1, 1] + [1] * 5) == "decode_reg_w16_nv4"
 
 
 # ----------------------------------------------------------------- GPU
@@ -100,6 +119,7 @@ gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
 @pytest.mark.parametrize("jit", ["1", "0"])
 @pytest.mark.parametrize("sb", [192, 8192])
 def test_low_rate_gpu_vs_oracle_and_roundtrip(oracle, monkeypatch, k, m, jit, sb):
+    """jit 1: networks where the map fits one kernel (else FFT form); jit 0: FFT form only."""
     monkeypatch.setenv("RS_AMD_JIT", jit)
     monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")  # every pass's network, not the table kernels of a pending compile
     dev = torch.device("cuda:0")
@@ -173,3 +193,58 @@ def test_low_rate_background_network(oracle, monkeypatch):
         assert (enc() == exp).all()
     R.net_wait()
     assert (enc() == exp).all()
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("k,m", LOW_KM_LARGE)
+@pytest.mark.parametrize("sb,n", [(4096, 2), (65536, 1)])
+def test_low_rate_large_codes(oracle, k, m, sb, n):
+    """Codes past the round-2 limit (k * m > 65536; chunk C = 256 / 512 / 1024, decode
+    transforms of W = 2048 / 8192 points): the generic FFT-form encode bit-exact against
+    the oracle's rso_encode_low, and the erasure-locator reconstruct restoring random
+    erasures (originals and recovery shards) bit-exact. Parity unpinned."""
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(k + m + sb)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev)
+    par = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
+    R.encode_batch_dev(k, m, d, par)
+    torch.cuda.synchronize()
+    got = par.cpu().numpy()
+    for s in range(n):
+        st, exp = oracle.encode_low(k, m, data[s])
+        assert st == 0
+        assert np.array_equal(got[s], exp), s
+    for e in (1, min(k, 97), k):
+        present = np.ones(k + m, np.uint8)
+        present[rng.choice(k, size=e, replace=False)] = 0
+        present[k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
+        missing = [i for i in range(k) if not present[i]]
+        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8, device=dev)
+        R.reconstruct_batch_dev(k, m, present, d, par, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), data[:, missing]), e
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("k,m", [(1, 65535), (64, 65472), (2, 40000)])
+def test_low_rate_widest_transforms(oracle, k, m):
+    """65,536-point decode transforms (W = ceilPow2(C + m) = 65536) on 64-byte shards."""
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(k + m)
+    sb = 64
+    data = rng.integers(0, 256, (1, k, sb), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev)
+    par = torch.zeros((1, m, sb), dtype=torch.uint8, device=dev)
+    R.encode_batch_dev(k, m, d, par)
+    torch.cuda.synchronize()
+    st, exp = oracle.encode_low(k, m, data[0])
+    assert st == 0 and np.array_equal(par.cpu().numpy()[0], exp)
+    present = np.zeros(k + m, np.uint8)  # every original lost, the last k recovery shards kept
+    present[k + m - k:] = 1
+    out = torch.zeros((1, k, sb), dtype=torch.uint8, device=dev)
+    R.reconstruct_batch_dev(k, m, present, d, par, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), data)
