@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--c4-reps", type=int, default=5,
-                    help="BASELINE configs[4] (RS(200,55) 256 KiB x 256) GPU leg after the timed region, N=1 (0 = skip)")
+                    help="BASELINE configs[4] (RS(200,55) 256 KiB x 512) GPU leg after the timed region, N=1 (0 = skip)")
+    ap.add_argument("--c4-stripes", type=int, default=512, help="stripes of the configs[4] leg (SURVEY.md §8(d): 512)")
     return ap.parse_args()
 
 
@@ -149,12 +150,15 @@ def _cpu_model():
     return "unknown"
 
 
-def c4_leg(dev, reps):
+def c4_leg(dev, reps, n=512):
     """BASELINE configs[4] on the GPU, outside the timed region (rank 0, N=1): RS(200,55)
-    256 KiB x 256 encode and reconstruct of 55 erased data shards (every third from 1), HIP
-    events over `reps` calls after a warm-up that includes the kernels' hipRTC compiles
-    (background compiles joined with net_wait). Restored shards are checked against the data."""
-    k, m, sb, n = 200, 55, 256 << 10, 256
+    256 KiB x n (512 stripes, 25 GiB of data) encode and reconstruct of 55
+    erased data shards (every third from 1), HIP events over `reps` calls after a warm-up
+    that includes the kernels' hipRTC compiles (background compiles joined with net_wait).
+    Then a cold pattern (every third from 2, never seen by the process): its first calls
+    timed without net_wait, as a repair service meeting a new pattern runs them. Restored
+    shards are checked against the data."""
+    k, m, sb = 200, 55, 256 << 10
     lost = list(range(1, k, 3))[:m]
     present = [0 if i in lost else 1 for i in range(k)] + [1] * m
     g = torch.Generator(device=dev)
@@ -167,7 +171,8 @@ def c4_leg(dev, reps):
         R.reconstruct_batch_dev(k, m, present, data, par, out)
     torch.cuda.synchronize()
     R.net_wait()
-    res = {"workload": "RS(200,55) 256 KiB shards x 256 stripes; reconstruct: 55 erased data shards (every third from 1)"}
+    res = {"workload": f"RS(200,55) 256 KiB shards x {n} stripes; reconstruct: 55 erased data shards "
+                       "(every third from 1)"}
     for name, fn, alg in (("encode", lambda: R.encode_batch_dev(k, m, data, par), (k + m) * sb * n),
                           ("reconstruct", lambda: R.reconstruct_batch_dev(k, m, present, data, par, out),
                            (k + m) * sb * n)):
@@ -184,6 +189,21 @@ def c4_leg(dev, reps):
                      "kernel": (R.encode_kernel_name(k, m, sb) if name == "encode"
                                 else R.reconstruct_kernel_name(k, m, sb, present))}
     res["verified"] = bool(torch.equal(out, data[:, lost]))
+    # cold pattern: first calls of an erasure pattern whose kernels are not compiled
+    lost_c = list(range(2, k, 3))[:m]
+    present_c = [0 if i in lost_c else 1 for i in range(k)] + [1] * m
+    calls = []
+    for _ in range(3):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        a.record()
+        R.reconstruct_batch_dev(k, m, present_c, data, par, out)
+        b.record()
+        torch.cuda.synchronize()
+        calls.append({"wall_ms": round((time.perf_counter() - t0) * 1e3, 3), "gpu_ms": round(a.elapsed_time(b), 3)})
+    res["reconstruct_cold"] = {"calls": calls, "pattern": "55 erased data shards, every third from 2",
+                               "note": "first calls of a new pattern, no net_wait (plan build included in wall_ms)",
+                               "verified": bool(torch.equal(out, data[:, lost_c]))}
     del data, par, out
     torch.cuda.empty_cache()
     return res
@@ -295,7 +315,7 @@ def main():
             del data, parity, restored
             torch.cuda.empty_cache()
             try:
-                c4 = c4_leg(dev, args.c4_reps)
+                c4 = c4_leg(dev, args.c4_reps, args.c4_stripes)
             except Exception as ex:  # never costs the headline line
                 c4 = {"error": str(ex)[:200]}
         out = {

@@ -13,6 +13,9 @@ int fail(int status, const std::string &msg) {
 }
 
 int hip_fail(hipError_t e, const char *what) {
+  // the failed call also set the thread's last HIP error: reset it, so the caller's next
+  // hipGetLastError (e.g. torch's launch check) does not report this call's failure
+  (void)hipGetLastError();
   return fail(RS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 

@@ -952,7 +952,7 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st, const uint32_t *dmask,
-                  uint32_t dmask_words) {
+                  uint32_t dmask_words, bool shared_mask) {
   if (n_stripes == 0) return hipSuccess;
   if (!supports(s.k, s.m, sb) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
     return hipErrorInvalidValue;
@@ -983,7 +983,7 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
   const unsigned char *d = data, *r = rec ? rec : data;
   unsigned char *o = out;
   const uint32_t *dm = dmask;
-  uint32_t dmw = dmask_words;
+  uint32_t dmw = shared_mask ? 0u : dmask_words;  // the kernel's per-stripe mask stride
   void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st, &dm, &dmw};
   return hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(grid), 1, 1, (C / 8) * 64, 1, 1, 0, st, args, nullptr);
 }

@@ -81,9 +81,11 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 
 // data [stripe][k][sb] (stride ds), rec [stripe][m][sb] (rs; read for kOutXorRec rows),
 // out [stripe][m][sb] (os; only the rows out_mode stores are written)
+// Spec::dyn: dmask = n_stripes blocks of dmask_words (or one block for every stripe:
+// shared_mask, a batch with one erasure pattern)
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st,
-                  const uint32_t *dmask = nullptr, uint32_t dmask_words = 0);
+                  const uint32_t *dmask = nullptr, uint32_t dmask_words = 0, bool shared_mask = false);
 
 // Host check of the generator's arithmetic: runs the kernel's schedule with its
 // T-coordinate matrices on scalar symbols and compares with scalar_encode.

@@ -129,6 +129,12 @@ struct DecodePlan {
   std::shared_ptr<DevBuf> skip;  // k-bit mask of the erased data shards
   std::shared_ptr<FftSlot> syn_fft;  // the syndromes' encode on the bit-sliced FFT kernel (wide codes)
   std::shared_ptr<FftSlot> inv_fft;  // every original lost, k == m == chunk: the encode inverted
+  // pattern-agnostic form of the syndrome path (wide codes), run while the pattern's own
+  // kernels compile: the code's FFT kernel with per-stripe masks (Spec::dyn, compiled once
+  // per code) + the generic e x e solve (rs_psyn.hpp) — one plan block for the batch
+  // (fftnet masks, then the solve header and A^-1 in polynomial form at word cold_dmw)
+  std::shared_ptr<DevBuf> cold;
+  uint32_t cold_dmw = 0, cold_pw = 0, cold_cs = 0;
 };
 
 // Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
@@ -212,6 +218,15 @@ int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *presen
 void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 
 // -------------------------------------------------------- patterns (rs_patterns.cpp)
+// Wide codes: the FFT kernel with per-stripe masks for the syndromes + the generic solve
+// (pattern-agnostic: compiled once per code; also the batch syndrome path's cold form)
+struct WpsSlot {
+  std::shared_ptr<FftSlot> fft = std::make_shared<FftSlot>();
+  std::mutex mu;
+  bool solve_failed = false;
+};
+void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<WpsSlot> &out);
+const jit::Kernel *wps_solve_kernel(WpsSlot &ws);
 // exp, log, log_walsh in HBM (384 KiB per device)
 int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw);
 

@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_low_generic(EncodeArgs a) {
       st(work + p * sb, v);
     }
     ifft_mem<NV>(work, sb, 0, C, a.k, a.tabs);
-    uint8_t *dst = a.parity + s * a.parity_stripe_stride;
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
     for (uint64_t j = 0; j < a.n_chunks; j++) {
       const uint64_t t = a.m - j * C < C ? a.m - j * C : C;
       for (uint64_t p = 0; p < C; p++) {

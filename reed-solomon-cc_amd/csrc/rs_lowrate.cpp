@@ -149,7 +149,8 @@ int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, std::share
   std::vector<RsTab> tabs;
   push_ifft_tabs(tabs, C, 0, false);
   for (uint64_t j = 0; j < p->n_chunks; j++) push_fft_tabs(tabs, C, (j + 1) * C, false);
-  if (int st = upload(tabs.data(), std::max<size_t>(1, tabs.size()) * sizeof(RsTab), dev, p->tabs)) return st;
+  if (tabs.empty()) tabs.push_back(make_twiddle(kModulus, false));  // C = 1: no butterflies
+  if (int st = upload(tabs.data(), tabs.size() * sizeof(RsTab), dev, p->tabs)) return st;
   if (net) {
     p->net = std::make_shared<NetSlot>();
     p->net->async = !jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(m), sb);

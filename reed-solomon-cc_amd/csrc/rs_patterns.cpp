@@ -33,6 +33,36 @@ int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uin
   return RS_OK;
 }
 
+std::map<std::string, std::shared_ptr<WpsSlot>> g_wps;
+
+void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<WpsSlot> &out) {
+  const std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
+                          std::to_string(flags & RS_FLAG_QUIRK_D2);
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  auto &p = g_wps[key];
+  if (!p) {
+    p = std::make_shared<WpsSlot>();
+    fftnet::Spec &fs = p->fft->spec;
+    fs.k = static_cast<uint32_t>(k);
+    fs.m = static_cast<uint32_t>(m);
+    fs.flags = flags & RS_FLAG_QUIRK_D2;
+    fs.dyn = true;
+  }
+  out = p;
+}
+
+const jit::Kernel *wps_solve_kernel(WpsSlot &ws) {
+  std::lock_guard<std::mutex> lk(ws.mu);
+  if (ws.solve_failed) return nullptr;
+  std::string err;
+  const jit::Kernel *sk = psyn::get_solve(cantor_basis(), err);
+  if (!sk) {
+    ws.solve_failed = true;
+    warn_once_per_reason("[rs_amd] per-stripe solve kernel unavailable, using table kernels: ", err);
+  }
+  return sk;
+}
+
 }  // namespace host
 }  // namespace rs
 
@@ -87,30 +117,6 @@ const jit::Kernel *psyn_kernel(PsynPlan &p) {
     warn_once_per_reason("[rs_amd] per-stripe syndrome network unavailable, using table kernels: ", err);
   }
   return k;
-}
-
-// Wide codes: the FFT kernel with per-stripe masks for the syndromes + the generic solve
-struct WpsSlot {
-  std::shared_ptr<FftSlot> fft = std::make_shared<FftSlot>();
-  std::mutex mu;
-  bool solve_failed = false;
-};
-std::map<std::string, std::shared_ptr<WpsSlot>> g_wps;
-
-void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<WpsSlot> &out) {
-  const std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                          std::to_string(flags & RS_FLAG_QUIRK_D2);
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  auto &p = g_wps[key];
-  if (!p) {
-    p = std::make_shared<WpsSlot>();
-    fftnet::Spec &fs = p->fft->spec;
-    fs.k = static_cast<uint32_t>(k);
-    fs.m = static_cast<uint32_t>(m);
-    fs.flags = flags & RS_FLAG_QUIRK_D2;
-    fs.dyn = true;
-  }
-  out = p;
 }
 
 // Under D2 a code with k > chunk and k % chunk == 0 drops its last full chunk
@@ -213,18 +219,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       wps_slot(dev, k, m, flags, ws);
       const fftnet::Spec *fs = nullptr;
       const jit::Kernel *fk = fft_kernel(*ws->fft, sb, &fs);
-      const jit::Kernel *sk = nullptr;
-      {
-        std::lock_guard<std::mutex> lk(ws->mu);
-        if (!ws->solve_failed) {
-          std::string err;
-          sk = psyn::get_solve(cantor_basis(), err);
-          if (!sk) {
-            ws->solve_failed = true;
-            warn_once_per_reason("[rs_amd] per-stripe solve kernel unavailable, using table kernels: ", err);
-          }
-        }
-      }
+      const jit::Kernel *sk = wps_solve_kernel(*ws);
       if (fk && sk) {
         hipStream_t s = static_cast<hipStream_t>(stream);
         // coefficients for min(max_e, m) outputs per syndrome, in groups of 8

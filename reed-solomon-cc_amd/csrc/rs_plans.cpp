@@ -173,6 +173,43 @@ int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &n
   return RS_OK;
 }
 
+// The cold form's plan block (rs_host.hpp DecodePlan::cold), the layout of the
+// per-stripe k_wps_plan blocks: fftnet::dyn mask words (erased data positions, then the
+// rows R stored), then at word dmw: [0] restored outputs, [1] e, [2 + i] = R_i,
+// [66 + i * cs + j] = A^-1[j][i] in polynomial form (from the syndrome map's blocks:
+// the image of the symbol 1 = the coefficient in Cantor coordinates).
+int cold_syndrome_block(int dev, uint64_t k, uint64_t m, const uint8_t *present, const jit::NetSpec &map,
+                        DecodePlan &plan) {
+  fftnet::Spec fs;
+  fs.k = static_cast<uint32_t>(k);
+  fs.m = static_cast<uint32_t>(m);
+  fs.dyn = true;
+  const uint32_t e = map.n_out, dmw = fftnet::dyn_mask_words(fs), cs = wps_coef_stride(e);
+  const uint32_t pw = dmw + 2 + 64 + 64 * cs;
+  std::vector<uint32_t> blk(pw, 0);
+  for (uint64_t i = 0; i < k; i++)
+    if (!present[i]) blk[i / 32] |= 1u << (i % 32);
+  const uint16_t *cantor = cantor_basis();
+  for (uint32_t i = 0; i < e; i++) {
+    const uint32_t r = static_cast<uint32_t>(map.src[i] & kSrcIndexMask);
+    blk[dmw - 2 + r / 32] |= 1u << (r % 32);
+    blk[dmw + 2 + i] = r;
+    for (uint32_t j = 0; j < e; j++) {
+      const uint16_t c = map.images[(static_cast<size_t>(i) * e + j) * 16];
+      uint32_t poly = 0;
+      for (int b = 0; b < 16; b++) poly ^= (c >> b & 1) ? cantor[b] : 0u;
+      blk[dmw + 2 + 64 + i * cs + j] = poly;
+    }
+  }
+  blk[dmw] = e;
+  blk[dmw + 1] = e;
+  if (int st = upload(blk.data(), blk.size() * sizeof(uint32_t), dev, plan.cold)) return st;
+  plan.cold_dmw = dmw;
+  plan.cold_pw = pw;
+  plan.cold_cs = cs;
+  return RS_OK;
+}
+
 // root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
 // kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
@@ -251,6 +288,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
         for (uint64_t i = 0; i < k; i++) fs.skip[i] = present[i] ? 0 : 1;
         fs.out_mode.assign(m, fftnet::kOutNone);
         for (int32_t src : map.src) fs.out_mode[src & kSrcIndexMask] = fftnet::kOutStore;
+        if (fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 && m <= 64)
+          if ((st = cold_syndrome_block(dev, k, m, present, map, *plan))) return st;
       }
     } else {
       reconstruct_map(k, m, flags, present, map);

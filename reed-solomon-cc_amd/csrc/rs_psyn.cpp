@@ -317,7 +317,7 @@ bool compile_check_solve(const uint16_t *cantor, std::string &err, double *ms, s
 
 hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_, const uint8_t *scratch, uint64_t ss,
                         uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
-                        uint32_t plan_dw, uint32_t hdr, uint32_t cs, hipStream_t st) {
+                        uint32_t plan_dw, uint32_t hdr, uint32_t cs, hipStream_t st, bool shared_plan) {
   if (n_stripes == 0) return hipSuccess;
   if (sb == 0 || sb % jit::kUnitBytes || sb >= (1ull << 32)) return hipErrorInvalidValue;
   if (cs == 0 || cs % kSolveMaxOut || cs > 64 || plan_dw < hdr + 2 + 64 + 64 * cs) return hipErrorInvalidValue;
@@ -329,7 +329,7 @@ hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_,
     unsigned char *o = out;
     uint64_t st0 = rs_, st1 = ss, so = so_, sbv = sb, first = s0;
     const uint32_t *pp = plan;
-    uint32_t pw = plan_dw, hd = hdr, c = cs;
+    uint32_t pw = shared_plan ? 0u : plan_dw, hd = hdr, c = cs;  // pw: the kernel's per-stripe plan stride
     void *args[] = {&a0, &st0, &a1, &st1, &o, &so, &sbv, &first, &pp, &pw, &hd, &c};
     hipError_t e = hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(gx), gy, groups, 256, 1, 1, 0, st, args, nullptr);
     if (e != hipSuccess) return e;

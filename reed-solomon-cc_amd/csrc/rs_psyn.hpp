@@ -67,9 +67,10 @@ constexpr uint32_t kSolveMaxOut = 8;
 std::string generate_solve(const uint16_t *cantor, const std::string &name);
 const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err);
 bool compile_check_solve(const uint16_t *cantor, std::string &err, double *ms, size_t *code_bytes);
+// shared_plan: one plan block for every stripe (a batch with one erasure pattern)
 hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_, const uint8_t *scratch, uint64_t ss,
                         uint8_t *out, uint64_t so_, uint64_t sb, uint64_t n_stripes, const uint32_t *plan,
-                        uint32_t plan_dw, uint32_t hdr, uint32_t cs, hipStream_t st);
+                        uint32_t plan_dw, uint32_t hdr, uint32_t cs, hipStream_t st, bool shared_plan = false);
 
 }  // namespace psyn
 }  // namespace rs

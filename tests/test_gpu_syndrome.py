@@ -131,3 +131,30 @@ def test_syndrome_fft_encode_vs_oracle(oracle, monkeypatch, k, m):
         name = R.reconstruct_kernel_name(k, m, sb, present)
         assert "fft_encode" in name, name
         assert (reconstruct(k, m, present, data, par) == data[:, missing]).all(), (k, m, sorted(lost), name)
+
+
+@pytest.mark.parametrize("k,m,e", [(200, 55, 55), (200, 55, 20), (100, 20, 12), (64, 64, 40), (40, 50, 33)])
+@pytest.mark.parametrize("net", ["async", "off"])
+def test_syndrome_cold_pattern_form(oracle, monkeypatch, k, m, e, net):
+    """A pattern whose own kernels are not loaded runs the pattern-agnostic form (the
+    code's FFT kernel with the batch's erasure mask + the generic e x e solve) instead of
+    the table kernels: first calls of fresh patterns, with the background network compile
+    pending (async) or disabled (off: the solve serves every call). Recovery shards are
+    lost too, so R is not a prefix of the rows."""
+    monkeypatch.delenv("RS_AMD_JIT_SYNC", raising=False)
+    monkeypatch.setenv("RS_AMD_DECODE", "syndrome")
+    if net == "off":
+        monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
+    rng = np.random.default_rng(k * 3 + m + e + (net == "off"))
+    sb, n = 8192, 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=8)
+    for trial in range(2):
+        lost = list(rng.choice(k, size=e, replace=False))
+        lost += [k + int(i) for i in rng.choice(m, size=min(m - e, 3), replace=False)]
+        present = np.ones(k + m, np.uint8)
+        present[lost] = 0
+        missing = [i for i in range(k) if not present[i]]
+        for call in range(2):
+            got = reconstruct(k, m, present, data, par)
+            assert (got == data[:, missing]).all(), (k, m, e, trial, call)
