@@ -44,7 +44,7 @@ typedef enum rs_status {
   RS_ERR_OUT_OF_MEMORY = 10,           /* allocator failure */
   RS_ERR_OVERFLOW = 11,                /* std.math.ceilPowerOfTwo */
   RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO"); here only per-stripe patterns */
-  RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* root.zig:385 @panic("TODO"); here only rs_reconstruct_batch_dev_patterns */
+  RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* root.zig:385 @panic("TODO"); no longer returned (tails are coded) */
   RS_ERR_INVALID_ARGUMENT = 14,        /* NULL pointer / bad stride */
   RS_ERR_DEVICE = 15,                  /* HIP runtime error (message: rs_last_error()) */
   RS_ERR_NO_DEVICE = 16,               /* no gfx950 device visible */
@@ -176,11 +176,12 @@ int rs_reconstruct_batch_host_multi(uint64_t original_count, uint64_t recovery_c
                                     int n_devices);
 
 /* Which device kernel a call would run on ("net_encode_i10_o4", "encode_reg_w4_nv4",
- * "decode_matrix_e4_nv4", "encode_generic_nv1", ...), assuming 16-byte aligned buffers.
- * present: k+m flags as for rs_reconstruct_batch_dev, or NULL for "the first min(k, m)
- * originals lost". net_<role>_* = bit-sliced XOR network generated for the plan and compiled
- * with hipRTC on first use (shard_bytes a multiple of 4096, <= 16 outputs; disable
- * with RS_AMD_JIT=0). */
+ * "decode_matrix_e4_nv4", "encode_generic_nv1", "net_fft_encode_i200_o55", ...), assuming
+ * 16-byte aligned buffers. present: k+m flags as for rs_reconstruct_batch_dev, or NULL for
+ * "the first min(k, m) originals lost". net_<role>_* = bit-sliced XOR network (or
+ * bit-sliced FFT kernel, net_fft_*) generated for the plan and compiled with hipRTC on
+ * first use (shards of 1 / 2 KiB or whole 4 KiB units, <= 64 outputs; up to 64 input blocks
+ * compile in the call, larger maps in the background; disable with RS_AMD_JIT=0). */
 const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
 const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                        const uint8_t *present);
@@ -211,11 +212,6 @@ int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules);
 int rs_net_compile_check(uint64_t original_count, uint64_t recovery_count, const uint8_t *present,
                          uint32_t flags, double *compile_ms);
 
-/* Bit-sliced FFT encode kernel (wide codes, chunk 32 / 64; DESIGN.md §3.5): generate
- * it for (original_count, recovery_count, flags) and compile it with hipRTC, without
- * loading it (a build check; no device needed). Optional outputs: compile time, code
- * object bytes, and the generated kernel's VALU instruction estimate per 2 KiB unit
- * (all waves). RS_ERR_INVALID_ARGUMENT if the code has no such kernel. */
 /* Generate the per-stripe syndrome-network reconstruct kernels of
  * rs_reconstruct_batch_dev_patterns (rs_psyn.hpp) and compile them with hipRTC (no
  * device): for k <= 64, m <= 4 the code's fixed k -> m syndrome network plus the
@@ -223,6 +219,11 @@ int rs_net_compile_check(uint64_t original_count, uint64_t recovery_count, const
  * per-stripe masks plus the generic solve. RS_ERR_INVALID_ARGUMENT if the code has none. */
 int rs_psyn_compile_check(uint64_t original_count, uint64_t recovery_count, uint32_t flags, double *compile_ms,
                           uint64_t *code_bytes);
+/* Bit-sliced FFT encode kernel (wide codes, chunk 32 / 64; DESIGN.md §3.5): generate
+ * it for (original_count, recovery_count, flags) and compile it with hipRTC, without
+ * loading it (a build check; no device needed). Optional outputs: compile time, code
+ * object bytes, and the generated kernel's VALU instruction estimate per 2 KiB unit
+ * (all waves). RS_ERR_INVALID_ARGUMENT if the code has no such kernel. */
 int rs_fft_compile_check(uint64_t original_count, uint64_t recovery_count, uint32_t flags, double *compile_ms,
                          uint64_t *code_bytes, uint64_t *valu_ops);
 /* Host check of that kernel's arithmetic (its butterfly schedule with its (u, v)

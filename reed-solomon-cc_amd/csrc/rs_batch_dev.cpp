@@ -14,7 +14,6 @@ namespace host {
 // Batches whose shard_bytes is not a multiple of 64 run on padded copies
 // ([stripe][shard][ceil(sb/64)*64], tail chunk in the reference's layout) in
 // slices of <= 1 GiB, then the outputs are unpadded.
-constexpr uint64_t kTailSliceBytes = 1ull << 30;
 
 int pad_shards(const uint8_t *src, uint64_t src_stripe_stride, uint64_t sb, uint8_t *dst, uint64_t dst_stripe_stride,
                uint64_t psb, uint64_t n, hipStream_t s) {

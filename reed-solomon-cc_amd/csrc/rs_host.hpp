@@ -206,6 +206,16 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
                     std::shared_ptr<DecodePlan> &out);
 
+// ------------------------------------------------------ shard tails (rs_batch_dev.cpp)
+// Batches whose shard_bytes is not a multiple of 64 run on padded copies
+// ([stripe][shard][ceil(sb/64)*64], the tail chunk in the layout root.zig:338-348 implies)
+// in slices of <= kTailSliceBytes.
+constexpr uint64_t kTailSliceBytes = 1ull << 30;
+int pad_shards(const uint8_t *src, uint64_t src_stripe_stride, uint64_t sb, uint8_t *dst, uint64_t dst_stripe_stride,
+               uint64_t psb, uint64_t n, hipStream_t s);
+int unpad_shards(const uint8_t *src, uint64_t src_stripe_stride, uint64_t sb, uint8_t *dst, uint64_t dst_stripe_stride,
+                 uint64_t n, hipStream_t s);
+
 // ---------------------------------------------------------- low rate (rs_lowrate.cpp)
 int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *orig, uint64_t ostride,
                uint8_t *rec, uint64_t rstride, uint32_t flags, int max_nv, hipStream_t s);

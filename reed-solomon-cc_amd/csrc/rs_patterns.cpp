@@ -175,11 +175,42 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     if (st) return st;
     if (n_stripes == 0 || max_e == 0) return RS_OK;
     if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");
-    if (sb % 64) return fail(RS_ERR_SHARD_TAIL_UNSUPPORTED, "per-stripe patterns need shard_bytes % 64 == 0");
     if (present_stride == 0) present_stride = k + m;
     if (orig_stride == 0) orig_stride = k * sb;
     if (rec_stride == 0) rec_stride = m * sb;
     if (out_stride == 0) out_stride = static_cast<uint64_t>(max_e) * sb;
+    if (sb % 64) {  // shard tails (root.zig:338-348 layout): padded copies, in slices
+      int dev;
+      if ((st = current_device(&dev))) return st;
+      hipStream_t s = static_cast<hipStream_t>(stream);
+      const uint64_t psb = (sb + 63) / 64 * 64, rows = k + m + max_e;
+      const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kTailSliceBytes / (rows * psb)));
+      void *buf = nullptr;
+      HIP_TRY(hipMallocAsync(&buf, cap * rows * psb, s));
+      uint8_t *po = static_cast<uint8_t *>(buf), *pr = po + cap * k * psb, *pout = pr + cap * m * psb;
+      const uint8_t *O = static_cast<const uint8_t *>(d_original), *Rc = static_cast<const uint8_t *>(d_recovery);
+      uint8_t *Out = static_cast<uint8_t *>(d_restored);
+      for (uint64_t s0 = 0; st == RS_OK && s0 < n_stripes; s0 += cap) {
+        const uint64_t cnt = std::min(cap, n_stripes - s0);
+        // every slot is padded (which are present varies per stripe; the kernels read only
+        // those), and the restored rows too, so the slots a stripe does not restore come
+        // back unchanged
+        for (uint64_t i = 0; st == RS_OK && i < k; i++)
+          st = pad_shards(O + s0 * orig_stride + i * sb, orig_stride, sb, po + i * psb, k * psb, psb, cnt, s);
+        for (uint64_t i = 0; st == RS_OK && i < m; i++)
+          st = pad_shards(Rc + s0 * rec_stride + i * sb, rec_stride, sb, pr + i * psb, m * psb, psb, cnt, s);
+        for (uint64_t j = 0; st == RS_OK && j < max_e; j++)
+          st = pad_shards(Out + s0 * out_stride + j * sb, out_stride, sb, pout + j * psb, max_e * psb, psb, cnt, s);
+        if (st == RS_OK)
+          st = rs_reconstruct_batch_dev_patterns(k, m, psb, cnt, d_present + s0 * present_stride, present_stride, max_e,
+                                                 po, 0, pr, 0, pout, 0, d_status ? d_status + s0 : nullptr, flags,
+                                                 stream);
+        for (uint64_t j = 0; st == RS_OK && j < max_e; j++)
+          st = unpad_shards(pout + j * psb, max_e * psb, sb, Out + s0 * out_stride + j * sb, out_stride, cnt, s);
+      }
+      (void)hipFreeAsync(buf, s);
+      return st;
+    }
     const int max_nv = align_nv({reinterpret_cast<uint64_t>(d_original), reinterpret_cast<uint64_t>(d_recovery),
                                  reinterpret_cast<uint64_t>(d_restored), orig_stride, rec_stride, out_stride});
     if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");

@@ -534,6 +534,35 @@ def test_shard_tails_vs_oracle(oracle, k, m, sb):
     assert (got == data[:, sorted(lost)]).all()
 
 
+@pytest.mark.parametrize("sb", [70, 1000, 4102])
+@pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (200, 55)])
+def test_per_stripe_patterns_shard_tails(oracle, k, m, sb):
+    """Per-stripe patterns with shard_bytes % 64 != 0 (root.zig:338-348 tail layout, as the
+    other entry points): every stripe restores its lost originals; restored slots past a
+    stripe's own e are left untouched."""
+    rng = np.random.default_rng(sb + k * 13)
+    n = 5
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = gpu_encode(k, m, data)
+    assert (par == oracle.encode_batch(k, m, data)).all()
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n):
+        e = int(rng.integers(0, min(k, m) + 1))
+        present[s, rng.choice(k, size=e, replace=False)] = 0
+        present[s, k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
+    max_e = min(k, m)
+    out = torch.full((n, max_e, sb), 0x5A, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    for s in range(n):
+        assert status[s] == 0, s
+        missing = [i for i in range(k) if not present[s, i]]
+        assert (out[s, :len(missing)] == data[s, missing]).all(), (s, missing)
+        assert (out[s, len(missing):] == 0x5A).all(), s
+
+
 def test_more_than_65535_stripes(oracle):
     """Launch splitting at 65535 stripes (grid y): network encode + reconstruct over
     65,540 stripes; the stripes either side of the split are checked against the oracle."""
