@@ -280,20 +280,18 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       ea.work = ep->work;
       ea.contig = contig_ok(sb, ke.nv);
       ea.skip = static_cast<const uint32_t *>(plan->skip->p);
+      // syndromes on the code's FFT kernel with the batch's mask block; the pattern's e x e
+      // network once its background compile has landed, the generic solve until then
+      // (DESIGN.md §3.3), the table kernels only without those
       const jit::Kernel *nk = plan->net && max_nv == 4 ? net_kernel(*plan->net, sb) : nullptr;
-      const fftnet::Spec *sfs = nullptr;
-      const jit::Kernel *fk = plan->syn_fft && max_nv == 4 ? fft_kernel(*plan->syn_fft, sb, &sfs) : nullptr;
-      // a pattern whose kernels are not loaded yet (they compile in the background) runs
-      // the pattern-agnostic form: the code's FFT kernel with the batch's erasure mask
-      // and/or the generic solve, not the table kernels
-      const bool cold_ok = plan->cold && max_nv == 4 && (!fk || !nk);
+      const bool blk = plan->syn_blk && max_nv == 4;
       const jit::Kernel *dk = nullptr, *sk = nullptr;
       const fftnet::Spec *dfs = nullptr;
-      if (cold_ok) {
+      if (blk) {
         std::shared_ptr<WpsSlot> ws;
         wps_slot(dev, k, m, 0, ws);
-        if (!fk) dk = fft_kernel(*ws->fft, sb, &dfs);
-        if (!nk && (fk || dk)) sk = wps_solve_kernel(*ws);
+        dk = fft_kernel(*ws->fft, sb, &dfs);
+        if (!nk && dk) sk = wps_solve_kernel(*ws);
       }
       // scratch per slice (RS_AMD_SYN_SLICE_MB, default 4096): a slice whose syndromes fit
       // the 256 MB Infinity Cache is read back by the map from there
@@ -316,13 +314,10 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
         db.xsrc_stripe_stride = m * sb;
         db.n_stripes = cnt;
         hipError_t err = hipSuccess;
-        const fftnet::Spec *fs = sfs;
-        const uint32_t *cold = cold_ok ? static_cast<const uint32_t *>(plan->cold->p) : nullptr;
-        if (fk)
-          err = fftnet::launch(*fk, *fs, eb.data, orig_stride, nullptr, 0, eb.parity, m * sb, sb, cnt, s);
-        else if (dk)  // the pattern's own FFT kernel is compiling: the code's, with the batch's mask
-          err = fftnet::launch(*dk, *dfs, eb.data, orig_stride, nullptr, 0, eb.parity, m * sb, sb, cnt, s, cold,
-                               plan->cold_pw, true);
+        const uint32_t *bk = blk ? static_cast<const uint32_t *>(plan->syn_blk->p) : nullptr;
+        if (dk)
+          err = fftnet::launch(*dk, *dfs, eb.data, orig_stride, nullptr, 0, eb.parity, m * sb, sb, cnt, s, bk,
+                               plan->syn_pw, true);
         else
           err = launch_encode(ke, eb, s);
         if (err == hipSuccess) {
@@ -331,7 +326,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
                               db.xsrc_stripe_stride);
           else if (sk)  // the e x e map is compiling: the generic solve on the same syndromes
             err = psyn::launch_solve(*sk, db.rec, rec_stride, db.xsrc, db.xsrc_stripe_stride, db.out, out_stride, sb,
-                                     cnt, cold, plan->cold_pw, plan->cold_dmw, plan->cold_cs, s, true);
+                                     cnt, bk, plan->syn_pw, plan->syn_dmw, plan->syn_cs, s, true);
           else
             err = launch_decode(kc, db, s);
         }

@@ -127,14 +127,14 @@ struct DecodePlan {
   // a scratch, then the e x e matrix kernel on rec ^ scratch rows (see syndrome_map)
   bool syndrome = false;
   std::shared_ptr<DevBuf> skip;  // k-bit mask of the erased data shards
-  std::shared_ptr<FftSlot> syn_fft;  // the syndromes' encode on the bit-sliced FFT kernel (wide codes)
   std::shared_ptr<FftSlot> inv_fft;  // every original lost, k == m == chunk: the encode inverted
-  // pattern-agnostic form of the syndrome path (wide codes), run while the pattern's own
-  // kernels compile: the code's FFT kernel with per-stripe masks (Spec::dyn, compiled once
-  // per code) + the generic e x e solve (rs_psyn.hpp) — one plan block for the batch
-  // (fftnet masks, then the solve header and A^-1 in polynomial form at word cold_dmw)
-  std::shared_ptr<DevBuf> cold;
-  uint32_t cold_dmw = 0, cold_pw = 0, cold_cs = 0;
+  // the syndrome path on wide codes (chunk 32 / 64, whole 4 KiB units): the code's FFT
+  // kernel with per-stripe masks (fftnet::Spec::dyn, compiled once per code) and, while
+  // the pattern's e x e network compiles, the generic solve (rs_psyn.hpp) — one plan block
+  // for the batch (fftnet masks, then at word syn_dmw the solve header and A^-1 in
+  // polynomial form)
+  std::shared_ptr<DevBuf> syn_blk;
+  uint32_t syn_dmw = 0, syn_pw = 0, syn_cs = 0;
 };
 
 // Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per

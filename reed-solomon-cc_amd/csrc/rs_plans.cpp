@@ -173,12 +173,12 @@ int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &n
   return RS_OK;
 }
 
-// The cold form's plan block (rs_host.hpp DecodePlan::cold), the layout of the
+// The syndrome path's plan block (rs_host.hpp DecodePlan::syn_blk), the layout of the
 // per-stripe k_wps_plan blocks: fftnet::dyn mask words (erased data positions, then the
 // rows R stored), then at word dmw: [0] restored outputs, [1] e, [2 + i] = R_i,
 // [66 + i * cs + j] = A^-1[j][i] in polynomial form (from the syndrome map's blocks:
 // the image of the symbol 1 = the coefficient in Cantor coordinates).
-int cold_syndrome_block(int dev, uint64_t k, uint64_t m, const uint8_t *present, const jit::NetSpec &map,
+int syndrome_block(int dev, uint64_t k, uint64_t m, const uint8_t *present, const jit::NetSpec &map,
                         DecodePlan &plan) {
   fftnet::Spec fs;
   fs.k = static_cast<uint32_t>(k);
@@ -203,10 +203,10 @@ int cold_syndrome_block(int dev, uint64_t k, uint64_t m, const uint8_t *present,
   }
   blk[dmw] = e;
   blk[dmw + 1] = e;
-  if (int st = upload(blk.data(), blk.size() * sizeof(uint32_t), dev, plan.cold)) return st;
-  plan.cold_dmw = dmw;
-  plan.cold_pw = pw;
-  plan.cold_cs = cs;
+  if (int st = upload(blk.data(), blk.size() * sizeof(uint32_t), dev, plan.syn_blk)) return st;
+  plan.syn_dmw = dmw;
+  plan.syn_pw = pw;
+  plan.syn_cs = cs;
   return RS_OK;
 }
 
@@ -276,21 +276,13 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
         if (!present[i]) bits[i / 32] |= 1u << (i % 32);
       if ((st = upload(bits.data(), bits.size() * sizeof(uint32_t), dev, plan->skip))) return st;
       plan->syndrome = true;
-      if (fft_enabled() && fftnet::supports(k, m, sb)) {
-        // Enc(d') on the FFT kernel: erased data shards read as zero, only the rows R stored
-        plan->syn_fft = std::make_shared<FftSlot>();
-        plan->syn_fft->async = true;
-        fftnet::Spec &fs = plan->syn_fft->spec;
-        fs.k = static_cast<uint32_t>(k);
-        fs.m = static_cast<uint32_t>(m);
-        fs.flags = RS_FLAG_CORRECTED;
-        fs.skip.assign(k, 0);
-        for (uint64_t i = 0; i < k; i++) fs.skip[i] = present[i] ? 0 : 1;
-        fs.out_mode.assign(m, fftnet::kOutNone);
-        for (int32_t src : map.src) fs.out_mode[src & kSrcIndexMask] = fftnet::kOutStore;
-        if (fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 && m <= 64)
-          if ((st = cold_syndrome_block(dev, k, m, present, map, *plan))) return st;
-      }
+      // Enc(d') on the code's FFT kernel with the batch's mask block (Spec::dyn: erased data
+      // read as zero, only the rows R stored): compiled once per code, as fast as a kernel
+      // specialised for the pattern (RS(200,55) losing 55: 6.59 vs 6.62 ms for the whole
+      // reconstruct, profiles/r03/synform.log), so no per-pattern FFT compile
+      if (fft_enabled() && fftnet::supports(k, m, sb) && fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
+          m <= 64)
+        if ((st = syndrome_block(dev, k, m, present, map, *plan))) return st;
     } else {
       reconstruct_map(k, m, flags, present, map);
     }
