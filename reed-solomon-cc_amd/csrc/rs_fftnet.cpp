@@ -633,8 +633,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     o << "  __builtin_amdgcn_sched_barrier(0);\n  {\n";
     if (!full) o << "  const u32 vm = " << mask_expr(vm) << ";\n";
     if (dyn)  // this wave's 8 positions of chunk j: one byte of the stripe's skip mask
-      o << "  const u32 dsk = (" << (std::string(rd) == "RDn" ? "DMn" : "DM") << "[" << j * C / 32
-        << "u + (w >> 2)] >> ((w & 3u) << 3)) & 0xFFu;\n";
+      o << "  const u32 dsk = (" << (std::string(rd) == "RDn" ? "DMn" : "DM") << "[(" << j * C
+        << "u + (w << 3)) >> 5] >> ((" << j * C << "u + (w << 3)) & 31u)) & 0xFFu;\n";
     for (uint32_t r = r0; r < r1; r++) {
       o << "  { const u32 so = (" << j * C + r << "u + (w << 3)) * sbl;\n    ";
       const std::string rd1 = std::string(rd) + "1";
@@ -861,10 +861,11 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
 
 }  // namespace
 
-bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
-  // chunk 16 (9 <= m <= 16, two waves per workgroup): RS_AMD_FFT_C16=0 keeps those codes
-  // on the networks
-  const uint64_t m_min = env_int("RS_AMD_FFT_C16", 0) ? 9 : 17;
+bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes, bool chunk16) {
+  // chunk 16 (9 <= m <= 16, two waves per workgroup): the per-stripe pattern path's
+  // syndromes (chunk16); encodes keep those codes on the networks (no faster there,
+  // DESIGN.md §3.5) unless RS_AMD_FFT_C16=1
+  const uint64_t m_min = chunk16 || env_int("RS_AMD_FFT_C16", 0) ? 9 : 17;
   if (!basis().ok || m < m_min || m > 64 || k == 0) return false;
   const uint64_t C = ceil_pow2(m);
   if (C != 16 && C != 32 && C != 64) return false;
@@ -954,7 +955,7 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st, const uint32_t *dmask,
                   uint32_t dmask_words, bool shared_mask) {
   if (n_stripes == 0) return hipSuccess;
-  if (!supports(s.k, s.m, sb) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
+  if (!supports(s.k, s.m, sb, s.dyn) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
     return hipErrorInvalidValue;
   if (s.dyn && (s.pieces != 1 || !dmask || dmask_words < dyn_mask_words(s))) return hipErrorInvalidValue;
   const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));

@@ -66,7 +66,7 @@ constexpr uint64_t kUnitBytes = 2048;  // shard bytes one workgroup covers per u
 // whole 2 KiB units (or 1 KiB: a unit spans two stripes) with k * shard_bytes below
 // 2 GiB (32-bit buffer offsets)
 constexpr uint32_t kMaxChunks = 16;
-bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes);
+bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes, bool chunk16 = false);
 uint32_t pieces(uint64_t shard_bytes);  // Spec::pieces for a shard size
 
 std::string generate(const Spec &s, const std::string &name);

@@ -137,7 +137,7 @@ hipError_t launch_pattern_matrix(const uint8_t *d_present, uint64_t present_stri
 
 // Per-stripe plan of the syndrome-network path (rs_psyn.hpp): G [m][k] encode
 // coefficients then the 16 Cantor basis elements (polynomial form); plan
-// [n][plan_dw] (k <= 64, m <= kPsynMaxM, max_out <= m)
+// [n][plan_dw] (k <= 256, m <= kPsynMaxM, max_out <= m; rs_psyn.hpp plan_dwords)
 constexpr uint32_t kPsynMaxM = 8;
 hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t max_out,
                             uint32_t max_e, uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log,

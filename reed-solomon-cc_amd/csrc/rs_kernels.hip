@@ -1275,9 +1275,10 @@ __global__ __launch_bounds__(256) void k_pattern_images(const uint8_t *__restric
 // E = the erased originals, R = the first e present recovery rows, A = G[R][E] (e x e
 // block of the code's encode coefficients, G[r][t] = parity r of data t = 1), and
 // x_E = A^-1 s_R with s_r = p_r ^ Enc_r(data, erased read as 0). Block per stripe
-// (u32): [0..1] erased mask, [2] R mask, [3] outputs stored = min(e, max_e) (0: none),
-// then [4 + r * max_out + j] = A^-1[j][i(r)] in polynomial coordinates (bit i: the
-// coefficient of alpha^i; 0 for rows outside R), the form the kernel multiplies in.
+// (u32, nw = ceil(k / 32)): [0, nw) erased mask, [nw] R mask, [nw + 1] outputs stored =
+// min(e, max_e) (0: none), then [nw + 2 + r * max_out + j] = A^-1[j][i(r)] in polynomial
+// coordinates (bit i: the coefficient of alpha^i; 0 for rows outside R), the form the
+// kernel multiplies in.
 // G: [m][k] coefficients followed by the 16 Cantor basis elements (polynomial form).
 __device__ __forceinline__ uint32_t gf_mul_d(uint32_t a, uint32_t b, const uint16_t *exp, const uint16_t *log) {
   return (a == 0 || b == 0) ? 0u : exp[add_mod_d(log[a], log[b])];
@@ -1292,15 +1293,16 @@ __global__ __launch_bounds__(64) void k_psyn_plan(const uint8_t *__restrict__ pr
   if (s >= n) return;
   const uint8_t *pr = present + s * present_stride;
   uint32_t *pl = plan + s * plan_dw;
+  const uint32_t nw = (k + 31) / 32;  // erased-original mask words (rs_psyn.hpp plan_dwords)
   uint32_t have = 0, e = 0;
   for (uint32_t i = 0; i < k + m; i++) have += pr[i] ? 1 : 0;
   for (uint32_t i = 0; i < k; i++) e += pr[i] ? 0 : 1;
   if (status) status[s] = have < k ? 2 : (e > max_e ? 14 : 0);  // as k_pattern_tables
-  pl[0] = pl[1] = pl[2] = pl[3] = 0;
+  for (uint32_t w = 0; w < nw + 2; w++) pl[w] = 0;
   if (have < k || e == 0) return;  // nothing restored (e <= present recovery <= m from here)
-  uint32_t E[kPsynMaxM], R[kPsynMaxM], em[2] = {0, 0}, rm = 0;
+  uint32_t E[kPsynMaxM], R[kPsynMaxM], rm = 0;
   for (uint32_t i = 0, c = 0; i < k && c < e; i++)
-    if (!pr[i]) E[c++] = i, em[i / 32] |= 1u << (i % 32);
+    if (!pr[i]) E[c++] = i;
   for (uint32_t r = 0, c = 0; r < m && c < e; r++)
     if (pr[k + r]) R[c++] = r, rm |= 1u << r;
   // Gauss-Jordan on [A | I] over GF(2^16)
@@ -1335,13 +1337,12 @@ __global__ __launch_bounds__(64) void k_psyn_plan(const uint8_t *__restrict__ pr
       const uint32_t c = (ir >= 0 && j < e) ? A[j][e + ir] : 0u;  // x_j += A^-1[j][i] s_{R_i}
       uint32_t poly = 0;
       for (int b = 0; b < 16; b++) poly ^= (c >> b & 1u) ? cantor[b] : 0u;
-      pl[4 + r * max_out + j] = poly;
+      pl[nw + 2 + r * max_out + j] = poly;
     }
   }
-  pl[0] = em[0];
-  pl[1] = em[1];
-  pl[2] = rm;
-  pl[3] = e < max_e ? e : max_e;
+  for (uint32_t i = 0; i < e; i++) pl[E[i] / 32] |= 1u << (E[i] % 32);
+  pl[nw] = rm;
+  pl[nw + 1] = e < max_e ? e : max_e;
 }
 
 // Per-stripe plan of the wide-code path (rs_psyn.hpp solve kernel after the FFT
@@ -1980,7 +1981,7 @@ hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uin
                             uint32_t max_e, uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log,
                             uint32_t *plan, uint32_t plan_dw, int32_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (k > 64 || m > kPsynMaxM || max_out > m || plan_dw < 4 + m * max_out) return hipErrorInvalidValue;
+  if (k > 256 || m > kPsynMaxM || max_out > m || plan_dw < (k + 31) / 32 + 2 + m * max_out) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_psyn_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present, present_stride,
                      k, m, max_out, max_e, n, G, d_exp, d_log, plan, plan_dw, status);
   return hipGetLastError();

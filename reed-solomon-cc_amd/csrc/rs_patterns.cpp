@@ -111,8 +111,9 @@ const jit::Kernel *psyn_kernel(PsynPlan &p) {
   std::lock_guard<std::mutex> lk(p.mu);
   if (p.failed) return nullptr;
   std::string err;
-  const jit::Kernel *k = psyn::get(p.spec, err);
-  if (!k) {
+  bool pending = false;
+  const jit::Kernel *k = psyn::get(p.spec, err, pending);
+  if (!k && !pending) {
     p.failed = true;
     warn_once_per_reason("[rs_amd] per-stripe syndrome network unavailable, using table kernels: ", err);
   }
@@ -132,7 +133,8 @@ bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t m
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
   return !(flags & RS_FLAG_QUIRK_D1) && !d2_drops_chunk(k, m, flags) &&
-         (mode.empty() || mode == "auto" || mode == "psyn") && fft_enabled() && fftnet::supports(k, m, sb) && fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
+         (mode.empty() || mode == "auto" || mode == "psyn") && fft_enabled() && fftnet::supports(k, m, sb, true) &&
+         fftnet::pieces(sb) == 1 && sb % jit::kUnitBytes == 0 &&
          m <= 64;  // max_e up to m: output groups of 8 (rs_psyn.hpp launch_solve)
 }
 

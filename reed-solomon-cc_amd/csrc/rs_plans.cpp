@@ -377,7 +377,7 @@ int rs_psyn_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compil
     if (is_low_rate(k, m) || (flags & RS_FLAG_QUIRK_D1))
       return fail(RS_ERR_INVALID_ARGUMENT, "no per-stripe syndrome network for this code");
     if (!psyn::supports(k, m, jit::kUnitBytes)) {
-      if (!fftnet::supports(k, m, jit::kUnitBytes))
+      if (!fftnet::supports(k, m, jit::kUnitBytes, true))
         return fail(RS_ERR_INVALID_ARGUMENT, "no per-stripe syndrome network for this code");
       // wide code: the FFT syndrome kernel with per-stripe masks + the generic solve
       fftnet::Spec fs;

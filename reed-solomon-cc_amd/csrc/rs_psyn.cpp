@@ -2,6 +2,7 @@
 #include "rs_psyn.hpp"
 
 #include <algorithm>
+#include <cctype>
 #include <cstdlib>
 #include <sstream>
 #include <utility>
@@ -12,7 +13,7 @@ namespace rs {
 namespace psyn {
 
 bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
-  return k >= 1 && k <= 64 && m >= 1 && m <= kMaxM && m <= kPsynMaxM && shard_bytes % jit::kUnitBytes == 0 &&
+  return k >= 1 && k <= kMaxK && m >= 1 && m <= kMaxM && m <= kPsynMaxM && shard_bytes % jit::kUnitBytes == 0 &&
          shard_bytes > 0 && k * shard_bytes < 0x80000000ull && m * shard_bytes < 0x80000000ull;
 }
 
@@ -28,7 +29,7 @@ int waves() { return std::max(0, std::min(8, env_int("RS_AMD_PSYN_WAVES", 3))); 
 bool skip_erased() { return env_int("RS_AMD_PSYN_SKIP", 1) != 0; }  // 3: 5.19 -> 5.07 ms (profiles/r02/patterns_psyn.jsonl)
 
 std::string key_of(const Spec &s) {
-  std::string k = "psyn:p" + std::to_string(prefetch()) + "w" + std::to_string(waves()) + "s" +
+  std::string k = "psyn2:p" + std::to_string(prefetch()) + "w" + std::to_string(waves()) + "s" +
                   std::to_string(skip_erased()) + ":" + std::to_string(s.k) +
                   ":" + std::to_string(s.m) + ":" + std::to_string(s.flags) + ":";
   k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
@@ -85,7 +86,7 @@ void emit_chain(std::ostringstream &o, uint32_t j) {
 }  // namespace
 
 std::string generate(const Spec &s, const std::string &name) {
-  const uint32_t K = s.k, M = s.m, MO = max_out(s.k, s.m), PDW = plan_dwords(s.k, s.m);
+  const uint32_t K = s.k, M = s.m, MO = max_out(s.k, s.m), PDW = plan_dwords(s.k, s.m), NW = mask_words(s.k);
   std::ostringstream o;
   // non-temporal loads and stores (every byte is touched once)
   o << "#define RS_NT 3\n" << jit::net_prelude();
@@ -94,7 +95,10 @@ std::string generate(const Spec &s, const std::string &name) {
        "  Raw x;\n  x.a0 = LDB(r, vo, so);\n  x.a1 = LDB(r, vo + 1024u, so);\n"
        "  x.b0 = LDB(r, vo + 2048u, so);\n  x.b1 = LDB(r, vo + 3072u, so);\n  return x;\n}\n";
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
-  if (waves()) o << "__attribute__((amdgpu_waves_per_eu(" << waves() << ", 8))) ";
+  // occupancy hint: 3 waves / SIMD for m <= 4 (168 VGPRs); 2 above (the 16 m syndrome
+  // planes stay live through the solve: a 3-wave cap spills ~2,900 VGPRs for RS(32,8))
+  const int wv = M <= 4 ? waves() : std::min(waves(), 2);
+  if (wv) o << "__attribute__((amdgpu_waves_per_eu(" << wv << ", 8))) ";
   o << "void " << name
     << "(const unsigned char *__restrict__ b0, u64 s0, const unsigned char *__restrict__ b1, u64 s1,\n"
        "    unsigned char *__restrict__ out, u64 so, u64 sb, u64 stripe0, const u32 *__restrict__ plan) {\n"
@@ -103,9 +107,11 @@ std::string generate(const Spec &s, const std::string &name) {
        "  const u64 unit = (u64)blockIdx.x * 4u + (threadIdx.x >> 6);\n"
        "  if (unit * 4096u >= sb) return;\n"
     << "  const u32 *pl = plan + s * " << PDW << "u;\n"
-    << "  const u32 ne = pl[3];\n"
+    << "  const u32 ne = pl[" << NW + 1 << "];\n"
        "  if (ne == 0u) return;\n"
-       "  const u32 em0 = pl[0], em1 = pl[1], rm = pl[2], sbl = (u32)sb;\n"
+    << "  const u32 rm = pl[" << NW << "], sbl = (u32)sb;\n";
+  for (uint32_t w = 0; w < NW; w++) o << "  const u32 em" << w << " = pl[" << w << "];\n";
+  o <<
        "  const u32 off = (u32)unit * 4096u + (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
        "  const __amdgpu_buffer_rsrc_t RZ = __builtin_amdgcn_make_buffer_rsrc((void *)b0, (short)0, 0, 0x00020000);\n"
     << "  const __amdgpu_buffer_rsrc_t RD = __builtin_amdgcn_make_buffer_rsrc((void *)(b0 + s * s0), (short)0, (int)("
@@ -138,7 +144,7 @@ std::string generate(const Spec &s, const std::string &name) {
     if (i >= n_inputs) return;
     o << "  const Raw R" << i << " = ";
     if (i < K)
-      o << "ldb(((" << (i < 32 ? "em0" : "em1") << " >> " << i % 32 << ") & 1u) ? RZ : RD, off, " << i << "u * sbl);\n";
+      o << "ldb(((em" << i / 32 << " >> " << i % 32 << ") & 1u) ? RZ : RD, off, " << i << "u * sbl);\n";
     else
       o << "ldb(((rm >> " << i - K << ") & 1u) ? RR : RZ, off, " << i - K << "u * sbl);\n";
   };
@@ -148,7 +154,7 @@ std::string generate(const Spec &s, const std::string &name) {
     // RS_AMD_PSYN_SKIP: an erased input (read as zeros) skips its transform and network
     // under a wave-uniform branch; its load stays unconditional (prefetch order)
     if (skip_erased())
-      o << "  if (!(" << (i < K ? std::string(i < 32 ? "(em0 >> " : "(em1 >> ") + std::to_string(i % 32) + ") & 1u"
+      o << "  if (!(" << (i < K ? "(em" + std::to_string(i / 32) + " >> " + std::to_string(i % 32) + ") & 1u"
                                 : "!((rm >> " + std::to_string(i - K) + ") & 1u)")
         << "))";
     o << "  {\n  u32 P[16];\n  planes(R" << i << ", P);\n";
@@ -172,36 +178,70 @@ std::string generate(const Spec &s, const std::string &name) {
   // x_j = sum_{r in R} A^-1[j][i(r)] s_r in polynomial coordinates: per syndrome the
   // chain X = s_r * alpha^i (x^16 = x^5 + x^3 + x^2 + 1), XORed into x_j where bit i of
   // the stripe's coefficient is set (wave-uniform branches)
-  o << "  u32 ";
-  for (uint32_t j = 0; j < MO; j++)
-    for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << " = 0u" << (j + 1 == MO && c == 15 ? ";\n" : ", ");
-  for (uint32_t r = 0; r < M; r++) {
-    o << "  if ((rm >> " << r << ") & 1u) {\n";
-    for (uint32_t j = 0; j < MO; j++) {
-      // one chain per (r, j): branches on one coefficient only (branches on several
-      // correlated conditions let the compiler thread and duplicate blocks)
-      o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << 4 + r * MO + j << "];\n  u32 ";
-      for (int c = 0; c < 16; c++) o << "X" << c << " = a" << r * 16 + c << (c == 15 ? ";\n" : ", ");
-      emit_chain(o, j);
-      o << "  }\n";
-    }
-    o << "  }\n  __builtin_amdgcn_sched_barrier(0);\n";
-  }
-  // back to Cantor coordinates (Cantor bit c = XOR of polynomial bits b with bit c of
-  // the inverse basis change's column b), then store
-  for (uint32_t j = 0; j < MO; j++) {
-    o << "  if (" << j << "u < ne) {\n  u32 P[16] = {";
+  auto store_out = [&](uint32_t j) {  // back to Cantor coordinates, then store
+    o << "  {\n  u32 P[16] = {";
     for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << (c == 15 ? "};\n" : ", ");
     o << "  u32 ";
-    for (int c = 0; c < 16; c++) o << "a" << c << (c == 15 ? ";\n" : ", ");
+    for (int c = 0; c < 16; c++) o << "z" << c << (c == 15 ? ";\n" : ", ");
     std::vector<uint16_t> rows(to_cantor, to_cantor + 16);
     std::vector<bool> oinit(16, false);
-    jit::emit_network_input(o, rows, oinit, static_cast<int>(1000 + j));
+    std::ostringstream net;
+    jit::emit_network_input(net, rows, oinit, static_cast<int>(1000 + j));
+    std::string code = net.str();  // the network writes a<c>: rename to z<c> (the syndromes live on)
+    for (int c = 15; c >= 0; c--) {
+      const std::string from = "a" + std::to_string(c), to = "z" + std::to_string(c);
+      for (size_t at = 0; (at = code.find(from, at)) != std::string::npos;) {
+        const bool word_start = at == 0 || !(std::isalnum(static_cast<unsigned char>(code[at - 1])) || code[at - 1] == '_');
+        const size_t end = at + from.size();
+        const bool word_end = end >= code.size() || !std::isdigit(static_cast<unsigned char>(code[end]));
+        if (word_start && word_end) {
+          code.replace(at, from.size(), to);
+          at += to.size();
+        } else {
+          at = end;
+        }
+      }
+    }
+    o << code;
     for (int c = 0; c < 16; c++)
-      if (!oinit[c]) o << "  a" << c << " = 0u;\n";
+      if (!oinit[c]) o << "  z" << c << " = 0u;\n";
     o << "  u32 Q[16] = {";
-    for (int c = 0; c < 16; c++) o << "a" << c << (c == 15 ? "};\n" : ", ");
+    for (int c = 0; c < 16; c++) o << "z" << c << (c == 15 ? "};\n" : ", ");
     o << "  st(O + " << j << "ull * sb + off, Q);\n  }\n";
+  };
+  if (M <= 4) {  // every output accumulates at once (16 MO + 16 M VGPRs)
+    o << "  u32 ";
+    for (uint32_t j = 0; j < MO; j++)
+      for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << " = 0u" << (j + 1 == MO && c == 15 ? ";\n" : ", ");
+    for (uint32_t r = 0; r < M; r++) {
+      o << "  if ((rm >> " << r << ") & 1u) {\n";
+      for (uint32_t j = 0; j < MO; j++) {
+        // one chain per (r, j): branches on one coefficient only (branches on several
+        // correlated conditions let the compiler thread and duplicate blocks)
+        o << "  if (" << j << "u < ne) {\n  const u32 cf = pl[" << NW + 2 + r * MO + j << "];\n  u32 ";
+        for (int c = 0; c < 16; c++) o << "X" << c << " = a" << r * 16 + c << (c == 15 ? ";\n" : ", ");
+        emit_chain(o, j);
+        o << "  }\n";
+      }
+      o << "  }\n  __builtin_amdgcn_sched_barrier(0);\n";
+    }
+    for (uint32_t j = 0; j < MO; j++) {
+      o << "  if (" << j << "u < ne)\n";
+      store_out(j);
+    }
+  } else {  // m in 5..8: one output at a time (16 M + 32 VGPRs for the solve)
+    for (uint32_t j = 0; j < MO; j++) {
+      o << "  if (" << j << "u < ne) {\n  u32 ";
+      for (int c = 0; c < 16; c++) o << "x" << j << "_" << c << " = 0u" << (c == 15 ? ";\n" : ", ");
+      for (uint32_t r = 0; r < M; r++) {
+        o << "  if ((rm >> " << r << ") & 1u) {\n  const u32 cf = pl[" << NW + 2 + r * MO + j << "];\n  u32 ";
+        for (int c = 0; c < 16; c++) o << "X" << c << " = a" << r * 16 + c << (c == 15 ? ";\n" : ", ");
+        emit_chain(o, j);
+        o << "  }\n";
+      }
+      store_out(j);
+      o << "  }\n  __builtin_amdgcn_sched_barrier(0);\n";
+    }
   }
   o << "}\n";
   return o.str();
@@ -337,10 +377,12 @@ hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_,
   return hipSuccess;
 }
 
-const jit::Kernel *get(const Spec &s, std::string &err) {
+const jit::Kernel *get(const Spec &s, std::string &err, bool &pending) {
   const std::string name = name_of(s);
-  bool pending = false;
-  return jit::get_source(key_of(s), name, [s, name] { return generate(s, name); }, false, err, pending);
+  // small kernels (RS(10,4): ~2 s of hipRTC) compile in the call; larger ones (RS(32,8):
+  // ~8 s) in the background while the caller takes its next path
+  const bool async = static_cast<uint64_t>(s.k + s.m) * ((s.m + 3) / 4) > 64;
+  return jit::get_source(key_of(s), name, [s, name] { return generate(s, name); }, async, err, pending);
 }
 
 bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_bytes) {

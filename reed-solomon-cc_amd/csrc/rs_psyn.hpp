@@ -32,7 +32,10 @@
 namespace rs {
 namespace psyn {
 
-constexpr uint32_t kMaxM = 4;  // syndrome + restored accumulators: 16 (m + min(k, m)) VGPRs
+// syndrome accumulators: 16 m VGPRs; restored outputs: all min(k, m) at once (16 each)
+// for m <= 4, one at a time for m in 5..8 (the syndromes stay in registers)
+constexpr uint32_t kMaxM = 8;
+constexpr uint32_t kMaxK = 256;  // erased-original mask words in the plan block
 
 struct Spec {
   uint32_t k = 0, m = 0, flags = 0;
@@ -42,12 +45,15 @@ struct Spec {
 
 // restored outputs a kernel computes per stripe (the plan's max_out)
 inline uint32_t max_out(uint32_t k, uint32_t m) { return k < m ? k : m; }
-// u32 words of one stripe's plan block (rs_internal.hpp launch_psyn_plan)
-inline uint32_t plan_dwords(uint32_t k, uint32_t m) { return 4 + m * max_out(k, m); }
+// u32 words of one stripe's plan block (rs_internal.hpp launch_psyn_plan): ceil(k / 32)
+// erased-original mask words, the R row mask, the outputs restored, then the coefficients
+inline uint32_t mask_words(uint32_t k) { return (k + 31) / 32; }
+inline uint32_t plan_dwords(uint32_t k, uint32_t m) { return mask_words(k) + 2 + m * max_out(k, m); }
 
 bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes);
 std::string generate(const Spec &s, const std::string &name);
-const jit::Kernel *get(const Spec &s, std::string &err);
+// nullptr with pending = true while a background compile runs (the caller takes another path)
+const jit::Kernel *get(const Spec &s, std::string &err, bool &pending);
 bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_bytes);
 
 // orig [stripe][k][sb] (stride os_), rec [stripe][m][sb] (rs_), out [stripe][..][sb]

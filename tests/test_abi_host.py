@@ -227,18 +227,28 @@ def test_patterns_path_selection(monkeypatch):
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_matrix" or \
         R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_fft"  # D1: no syndrome network
     assert R.patterns_kernel_name(10, 4, 2048, 4) == "pattern_matrix"  # below the 4 KiB unit
-    assert R.patterns_kernel_name(5, 5, 4096, 5) == "pattern_matrix"
+    assert R.patterns_kernel_name(5, 5, 4096, 5) == "psyn_k5_m5"
+    # mid-band codes (round 3): the fused syndrome network for k <= 256, m <= 8; chunk-16
+    # FFT syndromes + the generic solve for 9 <= m <= 16
+    assert R.patterns_kernel_name(100, 4, 1 << 20, 4) == "psyn_k100_m4"
+    assert R.patterns_kernel_name(32, 8, 1 << 20, 8) == "psyn_k32_m8"
+    assert R.patterns_kernel_name(40, 12, 1 << 20, 12) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(16, 16, 1 << 20, 16) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(64, 16, 1 << 20, 16) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(300, 8, 1 << 20, 8) in ("pattern_matrix", "pattern_fft")  # k > 256
     monkeypatch.setenv("RS_AMD_PATTERNS", "fft")
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "pattern_fft"
 
 
 def test_psyn_kernel_compiles_for_gfx950():
     """Per-stripe syndrome network (rs_psyn.hpp): generated and compiled per code; codes
-    outside its range (m > 4, D1 multiply, low rate) have none."""
+    outside its range (k > 256 with m <= 8, D1 multiply, low rate) have none."""
     assert R.psyn_compile_check(10, 4)["code_bytes"] > 10000
     assert R.psyn_compile_check(4, 2, 2)["code_bytes"] > 1000
+    assert R.psyn_compile_check(5, 5)["code_bytes"] > 10000  # m in 5..8: one output at a time
     assert R.psyn_compile_check(100, 20)["code_bytes"] > 10000  # wide: FFT with per-stripe masks + solve
-    for k, m, flags in ((5, 5, 0), (10, 4, 1), (2, 4, 0)):
+    assert R.psyn_compile_check(40, 12)["code_bytes"] > 10000  # chunk 16: the same, two waves per workgroup
+    for k, m, flags in ((300, 8, 0), (10, 4, 1), (2, 4, 0)):
         with pytest.raises(R.InvalidArgument):
             R.psyn_compile_check(k, m, flags)
 

@@ -517,6 +517,44 @@ def test_per_stripe_wide_codes(oracle, k, m, sb, n, flags, max_e):
         assert (out[s, len(got):] == 0xAB).all(), s
 
 
+@pytest.mark.parametrize("k,m,sb,n", [(100, 4, 8192, 7), (32, 8, 4096, 9), (64, 8, 8192, 5), (5, 5, 4096, 9),
+                                      (256, 5, 4096, 3), (40, 12, 8192, 6), (16, 16, 4096, 9), (64, 16, 4096, 5),
+                                      (9, 9, 4096, 7), (100, 10, 4096, 4)])
+@pytest.mark.parametrize("flags", [0, 2])
+@pytest.mark.parametrize("max_e", [4, 8, 16])
+def test_per_stripe_mid_band(oracle, monkeypatch, k, m, sb, n, flags, max_e):
+    """Mid-band codes on the per-stripe pattern path (round 3): the fused syndrome network
+    for k <= 256, m <= 8 (rs_psyn.hpp; m > 4 solves one output at a time) and chunk-16
+    FFT syndromes + the generic solve for 9 <= m <= 16. Stripes lose 0..max_e + 2
+    originals and random recovery shards; more than max_e restore the first max_e (14)."""
+    monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")  # the pattern kernels, not a pending compile's fallback
+    max_e = min(max_e, m)
+    path = R.patterns_kernel_name(k, m, sb, max_e, flags)
+    assert path in (f"psyn_k{k}_m{m}", "fft_syndromes+psyn_solve"), path
+    rng = np.random.default_rng(k * 11 + m + flags + max_e)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n - 1):
+        e = int(rng.integers(0, min(max_e + 2, m, k) + 1))
+        present[s, rng.choice(k, size=e, replace=False)] = 0
+        present[s, k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
+    present[n - 1, :] = 1
+    present[n - 1, : m + 1] = 0  # not enough shards
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    assert status[n - 1] == 2 and (out[n - 1] == 0xAB).all()
+    for s in range(n - 1):
+        missing = [i for i in range(k) if not present[s, i]]
+        assert status[s] == (14 if len(missing) > max_e else 0), s
+        got = missing[:max_e]
+        assert (out[s, :len(got)] == data[s, got]).all(), (s, missing)
+        assert (out[s, len(got):] == 0xAB).all(), s
+
+
 @pytest.mark.parametrize("sb", [2, 6, 66, 70, 1000, 4102])
 @pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (200, 55)])
 def test_shard_tails_vs_oracle(oracle, k, m, sb):
