@@ -530,6 +530,10 @@ def test_per_stripe_mid_band(oracle, monkeypatch, k, m, sb, n, flags, max_e):
     monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")  # the pattern kernels, not a pending compile's fallback
     max_e = min(max_e, m)
     path = R.patterns_kernel_name(k, m, sb, max_e, flags)
+    c = 1 << (m - 1).bit_length()
+    if flags & 2 and k > c and k % c == 0:  # D2 drops the last chunk: not MDS, the reference decode as written
+        assert path == "pattern_fft"
+        pytest.skip("D2-dropping code: covered against the oracle by test_reconstruct_per_stripe_patterns")
     assert path in (f"psyn_k{k}_m{m}", "fft_syndromes+psyn_solve"), path
     rng = np.random.default_rng(k * 11 + m + flags + max_e)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
