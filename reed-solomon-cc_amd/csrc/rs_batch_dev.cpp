@@ -293,10 +293,9 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
         dk = fft_kernel(*ws->fft, sb, &dfs);
         if (!nk && dk) sk = wps_solve_kernel(*ws);
       }
-      // scratch per slice (RS_AMD_SYN_SLICE_MB, default 4096): a slice whose syndromes fit
-      // the 256 MB Infinity Cache is read back by the map from there
-      const char *sl = std::getenv("RS_AMD_SYN_SLICE_MB");
-      const uint64_t cap = (sl && *sl ? std::max(1, std::atoi(sl)) : 4096) * (1ull << 20);
+      // syndrome scratch in slices of <= 4 GiB (slices small enough for the 256 MB Infinity
+      // Cache measured slower: less work per launch)
+      const uint64_t cap = 4096ull << 20;
       const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, cap / (m * sb)));
       void *scratch = nullptr;
       HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));

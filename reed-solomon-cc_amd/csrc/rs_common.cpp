@@ -107,8 +107,7 @@ const jit::Kernel *fft_kernel(FftSlot &slot, uint64_t sb, const fftnet::Spec **u
   *used = &spec;
   std::string err;
   bool pending = false;
-  const char *a = std::getenv("RS_AMD_FFT_ASYNC");
-  const bool async = a && *a ? std::strcmp(a, "0") != 0 : slot.async;
+  const bool async = slot.async;
   const jit::Kernel *k = fftnet::get(spec, async, err, pending);
   if (!k && !pending) {
     slot.failed[vi] = true;

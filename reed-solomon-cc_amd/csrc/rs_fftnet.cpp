@@ -274,8 +274,6 @@ int env_int(const char *name, int def) {
   return e && *e ? std::atoi(e) : def;
 }
 
-int nt_of() { return env_int("RS_AMD_FFT_NT", 3) & 3; }
-bool blocked_of() { return env_int("RS_AMD_FFT_BLOCKED", 0) != 0; }
 
 int prefetch_of(const Spec &s) {
   return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", 4)));
@@ -507,29 +505,22 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   Plan P = make_plan(s);
   Gen g;
   g.st = stats;
-  g.sched = env_int("RS_AMD_FFT_SCHED", 1);
+  g.sched = 1;  // sched_barrier per butterfly: bounds the scheduler's interleaving (compile time)
   Stats dummy;
   if (!g.st) g.st = &dummy;
   std::ostringstream &o = g.o;
   const uint32_t NW = P.NW, C = P.C;
   bool any_xor = false;
   for (uint32_t q = 0; q < s.m; q++) any_xor |= P.out_mode[q] == kOutXorRec;
-  // RS_AMD_FFT_NT: non-temporal loads (bit 0) / stores (bit 1) (cache policy bit nt = 2);
-  // default both: RS(200,55) 256 KiB encode 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
-  const int nt = nt_of();
-  const bool blocked = blocked_of();
+  // non-temporal loads and stores (cache policy bit nt = 2): RS(200,55) 256 KiB encode
+  // 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
   const bool dyn = s.dyn;
-  o << "#define RS_AUX_LD " << ((nt & 1) ? 2 : 0) << "\n#define RS_AUX_ST " << ((nt & 2) ? 2 : 0) << "\n" << kPrelude;
+  o << "#define RS_AUX_LD 2\n#define RS_AUX_ST 2\n" << kPrelude;
   // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
   // batch, so its loads read zeros and its stores are dropped)
   const bool two = s.pieces == 2;
-  // RS_AMD_FFT_DEBUG_NOMEM (measurement aid, wrong bytes): bit 0 reads data through the
-  // zero-record resource (no load traffic), bit 1 drops the stores the same way
-  const int nomem = env_int("RS_AMD_FFT_DEBUG_NOMEM", 0);
   auto rsrc = [&](const char *base, const char *stride, const std::string &stripe, uint32_t rows) {
-    if (((nomem & 1) && std::string(base) == "data") || ((nomem & 2) && std::string(base) == "out"))
-      return std::string("RZ");
     return std::string("__builtin_amdgcn_make_buffer_rsrc((void *)(") + base + " + (" + stripe + ") * " + stride +
            "), (short)0, (int)(" + std::to_string(rows) + "u * sbl), 0x00020000)";
   };
@@ -555,17 +546,11 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
        "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
-       // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division in the loop);
-       // RS_AMD_FFT_BLOCKED: workgroup b takes the contiguous units [b * per, b * per + per)
-       << (blocked ? "  const u64 per = (n_units + gridDim.x - 1) / gridDim.x, ub = blockIdx.x * per,\n"
-                     "            ue = ub + per < n_units ? ub + per : n_units;\n"
-                     "  u64 stripe = ub / ups;\n"
-                     "  u32 uu = (u32)(ub - stripe * ups);\n"
-                     "  const u32 gdiv = 0u, gmod = 1u;\n"
-                   : "  const u64 ub = blockIdx.x, ue = n_units;\n"
-                     "  u64 stripe = blockIdx.x / ups;\n"
-                     "  u32 uu = blockIdx.x - (u32)stripe * ups;\n"
-                     "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n")
+       // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division in the loop)
+       "  const u64 ub = blockIdx.x, ue = n_units;\n"
+       "  u64 stripe = blockIdx.x / ups;\n"
+       "  u32 uu = blockIdx.x - (u32)stripe * ups;\n"
+       "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n"
     << 
        "  const __amdgpu_buffer_rsrc_t RZ = __builtin_amdgcn_make_buffer_rsrc((void *)data, (short)0, 0, 0x00020000);\n"
        "  v4 la0[8], lb0[8];\n"
@@ -577,7 +562,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // (loads emitted below, once emit_loads exists)
   std::ostringstream hdr2;
   hdr2 << "#pragma unroll 1\n"
-    << (blocked ? "  for (u64 u = ub; u < ue; u++) {\n" : "  for (u64 u = ub; u < ue; u += gridDim.x) {\n")
+    << "  for (u64 u = ub; u < ue; u += gridDim.x) {\n"
     << 
        "  u32 sbl = sb;\n"
        "  asm volatile(\"\" : \"+s\"(sbl));  // shard offsets are recomputed per unit (SALU), not hoisted into VGPRs\n"
@@ -590,30 +575,20 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   for (uint32_t r = 0; r < 8; r++)
     for (int i = 0; i < 8; i++) hdr2 << "w" << r << "_" << i << ", b" << r << "_" << i << ", c" << r << "_" << i << (r == 7 && i == 7 ? ";\n" : ", ");
 
-  // LDS slot accesses (RS_AMD_FFT_LDS128: 4-dword accesses, planes 4q..4q+3 of a slot
-  // in quad q — the default, 3.77 -> 3.54 ms on RS(200,55) in spite of 17 more VGPRs for
-  // the 4-register tuples; else dword accesses, plane i at (s * 8 + i) * 64)
-  const bool l128 = env_int("RS_AMD_FFT_LDS128", 1) != 0;
+  // LDS slot accesses: 4-dword accesses, planes 4q..4q+3 of a slot in quad q (dword
+  // accesses measured 3.77 vs 3.54 ms on RS(200,55) in spite of 17 more VGPRs for the
+  // 4-register tuples)
   auto lds_write = [&](const std::string &wexpr, uint32_t slot, const std::vector<std::string> &v) {
     // slot address = wexpr (runtime, in slots) + slot
-    for (int q = 0; q < (l128 ? 2 : 8); q++) {
-      if (l128)
-        o << "  xch4[lq + " << wexpr << " * 128u + " << slot * 128 + q * 64 << "u] = (v4){" << v[4 * q] << ", "
-          << v[4 * q + 1] << ", " << v[4 * q + 2] << ", " << v[4 * q + 3] << "};\n";
-      else
-        o << "  xch[lq + " << wexpr << " * 512u + " << (slot * 8 + q) * 64 << "u] = " << v[q] << ";\n";
-    }
+    for (int q = 0; q < 2; q++)
+      o << "  xch4[lq + " << wexpr << " * 128u + " << slot * 128 + q * 64 << "u] = (v4){" << v[4 * q] << ", "
+        << v[4 * q + 1] << ", " << v[4 * q + 2] << ", " << v[4 * q + 3] << "};\n";
   };
   auto lds_read = [&](const std::string &wexpr, uint32_t slot, const std::vector<std::string> &v) {
-    if (l128) {
-      o << "  { const v4 q0 = xch4[lq + " << wexpr << " * 128u + " << slot * 128 << "u], q1 = xch4[lq + " << wexpr
-        << " * 128u + " << slot * 128 + 64 << "u];\n";
-      for (int i = 0; i < 4; i++) o << "  " << v[i] << " = q0[" << i << "]; " << v[4 + i] << " = q1[" << i << "];\n";
-      o << "  }\n";
-    } else {
-      for (int i = 0; i < 8; i++)
-        o << "  " << v[i] << " = xch[lq + " << wexpr << " * 512u + " << (slot * 8 + i) * 64 << "u];\n";
-    }
+    o << "  { const v4 q0 = xch4[lq + " << wexpr << " * 128u + " << slot * 128 << "u], q1 = xch4[lq + " << wexpr
+      << " * 128u + " << slot * 128 + 64 << "u];\n";
+    for (int i = 0; i < 4; i++) o << "  " << v[i] << " = q0[" << i << "]; " << v[4 + i] << " = q1[" << i << "];\n";
+    o << "  }\n";
   };
 
   // ---- loads of chunk j (layout A: wave w reads positions w*8 + r), raw into la/lb
@@ -653,12 +628,11 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // RS_AMD_FFT_PREFETCH: positions of the next chunk loaded before this chunk's layers
   // (the rest just before their plane transform)
   const uint32_t pf = static_cast<uint32_t>(prefetch_of(s));
-  // RS_AMD_FFT_XUNIT: the next unit's first pf positions are loaded during this unit's FFT
-  const bool xunit = env_int("RS_AMD_FFT_XUNIT", 1) != 0;
+  // the next unit's first pf positions are loaded during this unit's FFT
   declared[0] = 1;  // la0 / lb0 live across units (cross-unit prefetch)
-  std::vector<uint32_t> vm_next = emit_loads(0, 0, xunit ? pf : 0);
+  std::vector<uint32_t> vm_next = emit_loads(0, 0, pf);
   o << "  }\n" << hdr2.str();
-  emit_loads(0, xunit ? pf : 0, 8);
+  emit_loads(0, pf, 8);
   for (size_t j = 0; j < P.truncs.size(); j++) {
     const std::vector<uint32_t> vm = vm_next;
     if (j > 0) emit_loads(j, pf, 8);
@@ -779,11 +753,10 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   }
   // the next unit's leading chunk-0 positions, in flight during this unit's last exchange and stores
   o << "  u64 stripe_n = stripe + gdiv;\n  u32 uu_n = uu + gmod;\n  if (uu_n >= ups) { uu_n -= ups; stripe_n++; }\n";
-  if (pf && xunit) {
+  if (pf) {
     o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = " << (two ? "loff" : "uon + 1024u") << ";\n";
-    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, blocked ? "u + 1u < ue" : "u + gridDim.x < ue");
-    if (dyn) o << "  const u32 *DMn = dm + ((" << (blocked ? "u + 1u < ue" : "u + gridDim.x < ue")
-               << ") ? stripe_n : 0ull) * dmw;\n";
+    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, "u + gridDim.x < ue");
+    if (dyn) o << "  const u32 *DMn = dm + ((u + gridDim.x < ue) ? stripe_n : 0ull) * dmw;\n";
     emit_loads(0, 0, pf, "RDn", "uon", "uon1");
     o << "  }\n";
   }
@@ -864,8 +837,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
 bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes, bool chunk16) {
   // chunk 16 (9 <= m <= 16, two waves per workgroup): the per-stripe pattern path's
   // syndromes (chunk16); encodes keep those codes on the networks (no faster there,
-  // DESIGN.md §3.5) unless RS_AMD_FFT_C16=1
-  const uint64_t m_min = chunk16 || env_int("RS_AMD_FFT_C16", 0) ? 9 : 17;
+  // DESIGN.md §3.5)
+  const uint64_t m_min = chunk16 ? 9 : 17;
   if (!basis().ok || m < m_min || m > 64 || k == 0) return false;
   const uint64_t C = ceil_pow2(m);
   if (C != 16 && C != 32 && C != 64) return false;
@@ -885,10 +858,7 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
-  std::string k = "fft:p" + std::to_string(prefetch_of(s)) + "n" + std::to_string(nt_of()) + "s" +
-                  std::to_string(env_int("RS_AMD_FFT_SCHED", 1)) + "l" + std::to_string(env_int("RS_AMD_FFT_LDS128", 1)) +
-                  "x" + std::to_string(env_int("RS_AMD_FFT_XUNIT", 1)) + "b" + std::to_string(blocked_of()) +
-                  (env_int("RS_AMD_FFT_DEBUG_NOMEM", 0) ? "nomem" + std::to_string(env_int("RS_AMD_FFT_DEBUG_NOMEM", 0)) : "") + ":" +
+  std::string k = "fft3:p" + std::to_string(prefetch_of(s)) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +

@@ -234,23 +234,20 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
   }
 }
 
-// Code-shape knobs (env, read at generation time; part of the cache key):
-//   RS_AMD_NET_PREFETCH  inputs loaded ahead of the one being transformed (default 0;
-//                        the compiler hoists the loads anyway)
-//   RS_AMD_NET_WAVES     amdgpu_waves_per_eu occupancy hint, 0 = none (default 0)
-//   RS_AMD_NET_NT        non-temporal loads (bit 0) / stores (bit 1), default 3 for
-//                        one output tile, 2 for several (their inputs are re-read)
-//   RS_AMD_NET_UNITS     4 KiB units per wave, walked in a loop (default 1)
+// Code shape. Constants measured in rounds 1-2 (profiles/r01/sweep_net_*.jsonl): no input
+// prefetch (the compiler hoists the loads anyway), no occupancy hint, non-temporal loads
+// and stores for one-tile maps (stores only for several tiles: their inputs are re-read
+// through L2), one 4 KiB unit per wave, sched_barriers between inputs above 16 input
+// blocks (bounds the scheduling regions: compile time stays ~linear in size). The knobs
+// the tests use to reach the other forms (read at generation time, part of the cache key):
 //   RS_AMD_NET_TILE      outputs per workgroup, 4 (64 accumulator planes) or 8 (default:
 //                        half the input re-reads and plane transforms of multi-tile maps;
 //                        RS(32,8) encode 2.39 -> 1.91 ms, the 55 x 55 syndrome map
 //                        13.9 -> 12.3 ms reconstruct, profiles/r01/sweep_net_tile8.jsonl)
-//   RS_AMD_NET_BARRIER   sched_barrier between inputs: bounds the scheduling regions,
-//                        so compile time stays ~linear in size (1 on, 0 off, default
-//                        -1: on above 16 input blocks; off costs nothing to compile
-//                        for small networks and measured ~1.5% faster on RS(10,4))
+//   RS_AMD_NET_SHARED    0: the classic form instead of the shared-input form
+//   RS_AMD_NET_BALANCE   0: one wave per 8-output tile in the shared form
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, shared_batch = 1, balance = 1;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, balance = 1;
 };
 
 int env_int(const char *name, int def) {
@@ -260,23 +257,14 @@ int env_int(const char *name, int def) {
 
 Tuning tuning() {
   Tuning t;
-  t.prefetch = std::max(0, std::min(8, env_int("RS_AMD_NET_PREFETCH", t.prefetch)));
-  t.waves = std::max(0, std::min(8, env_int("RS_AMD_NET_WAVES", t.waves)));
-  t.nt = env_int("RS_AMD_NET_NT", t.nt) & 3;
-  t.barrier = env_int("RS_AMD_NET_BARRIER", t.barrier);
-  t.units = std::max(1, std::min(64, env_int("RS_AMD_NET_UNITS", t.units)));
   t.tile = env_int("RS_AMD_NET_TILE", t.tile) >= 8 ? 8 : 4;
   t.shared = env_int("RS_AMD_NET_SHARED", t.shared);
-  t.shared_batch = env_int("RS_AMD_NET_SHARED_BATCH", t.shared_batch);
   t.balance = env_int("RS_AMD_NET_BALANCE", t.balance) != 0;
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
-  return "p" + std::to_string(t.prefetch) + "w" + std::to_string(t.waves) + "n" + std::to_string(t.nt) + "b" +
-         std::to_string(t.barrier) + "u" + std::to_string(t.units) + "t" + std::to_string(t.tile) + "s" +
-         std::to_string(t.shared) + (t.shared_batch != 1 ? "x" + std::to_string(t.shared_batch) : "") +
-         (t.balance ? "" : "nb");
+  return "t" + std::to_string(t.tile) + "s" + std::to_string(t.shared) + (t.balance ? "" : "nb");
 }
 
 // Shared-input form (generate_shared): one workgroup of n_tiles waves per 4 KiB unit,
@@ -312,10 +300,7 @@ void emit_network_input(std::ostringstream &o, const std::vector<uint16_t> &rows
   emit_input(o, rows, init, t);
 }
 
-uint64_t max_blocks() {
-  const int v = env_int("RS_AMD_NET_MAX_BLOCKS", 0);
-  return v > 0 ? static_cast<uint64_t>(v) : kMaxBlocks;
-}
+uint64_t max_blocks() { return kMaxBlocks; }
 
 bool supports(uint32_t n_in, uint32_t n_out, uint64_t shard_bytes) {
   const uint64_t blocks = static_cast<uint64_t>(n_in) * ((n_out + kTileOut - 1) / kTileOut);
@@ -347,15 +332,15 @@ namespace {
 // is read from HBM and transposed once instead of once per tile.
 std::string generate_shared(const NetSpec &spec, const std::string &name, const Tuning &tu) {
   const uint32_t n_in = spec.n_in, n_out = spec.n_out;
-  // RS_AMD_NET_SHARED_BATCH: inputs staged per wave between barriers (batch = T * mult)
-  // (two buffers of 4 KiB per staged input within the 160 KiB of LDS)
+  // one input staged per wave between barriers (two staged inputs per wave measured slower:
+  // 8.25 vs 6.84 ms on the c4 55 x 55 map, 240 VGPRs)
   const uint32_t T = shared_tiles(tu, spec);
   // tile w owns outputs [w * n_out / T, (w + 1) * n_out / T)
   auto tile_first = [&](uint32_t w) { return static_cast<uint32_t>(static_cast<uint64_t>(w) * n_out / T); };
-  const uint32_t mult = std::max(1u, std::min({4u, static_cast<uint32_t>(std::max(1, tu.shared_batch)), 20u / T}));
+  const uint32_t mult = 1;
   const uint32_t BW = T * mult, nb = (n_in + BW - 1) / BW;
   std::ostringstream o;
-  o << "#define RS_NT " << (std::getenv("RS_AMD_NET_NT") ? tu.nt : 3) << "\n" << kPrelude;
+  o << "#define RS_NT " << tu.nt << "\n" << kPrelude;
   o << "extern \"C\" __global__ __launch_bounds__(" << 64 * T << ") ";
   if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
   o << "void " << name
@@ -448,7 +433,7 @@ std::string generate_with(const NetSpec &spec, const std::string &name, const Tu
   std::ostringstream o;
   // several output tiles re-read every input through L2: non-temporal loads (which
   // evict early) cost 10-15 % there, so by default they are kept for 1-tile maps only
-  const int nt = std::getenv("RS_AMD_NET_NT") || n_tiles == 1 ? tu.nt : (tu.nt & 2);
+  const int nt = n_tiles == 1 ? tu.nt : (tu.nt & 2);
   const uint32_t P = spec.pieces;  // stripes per wave unit (1, or 2 / 4 for 2 / 1 KiB shards)
   o << "#define RS_NT " << nt << "\n" << kPrelude;
   if (P > 1) o << kPreludeSmall;

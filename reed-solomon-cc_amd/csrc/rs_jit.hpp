@@ -45,7 +45,7 @@ constexpr uint32_t kTileOut = 4;      // size caps count blocks of one input x 4
 constexpr uint32_t kMaxOut = 64;      // tiles of 8 outputs (RS_AMD_NET_TILE), one workgroup each
 // generated code size: n_in x tiles input blocks of ~270 instructions each; hipRTC
 // takes ~20-40 ms per block, so the cap keeps a plan's compile near 1-2 s
-// (RS_AMD_NET_MAX_BLOCKS overrides it, see max_blocks())
+// (max_blocks())
 constexpr uint64_t kMaxBlocks = 64;
 uint64_t max_blocks();
 // Larger maps (the e x e syndrome map of wide codes: RS(200,55) losing 55 is 770

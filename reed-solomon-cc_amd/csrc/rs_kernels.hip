@@ -374,120 +374,10 @@ __global__ __launch_bounds__(kBlock) void k_encode_ws64l(EncodeArgs a) {
   }
 }
 
-// PF: chunk c+1's loads are issued right after chunk c's are paired, so they are in
-// flight during chunk c's butterflies and LDS transposes (+16 dword pairs per lane).
-template <int NV, bool SHARED, bool PF>
-__global__ __launch_bounds__(kBlock) void k_encode_ws64(EncodeArgs a) {
-  constexpr int TI = 63;  // ifft_tab_count(64): 16 + 4 + 1 groups x 3
-  __shared__ LdsSym<NV> lds[64][64];
-  const uint64_t sb = a.shard_bytes;
-  const uint64_t regions = sb / 64 * (8 / NV) / 64;
-  if (blockIdx.x >= regions) return;  // whole block: every wave shares the region
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
-  {  // one stripe per blockIdx.y (launches are split at 65535 stripes)
-    const uint64_t s = blockIdx.y;
-    const uint8_t *src = a.data + s * a.data_stripe_stride;
-    auto trunc_of = [&](uint32_t c) { return c == 0 ? a.trunc_first : (c + 1 == a.n_chunks ? a.trunc_last : 64u); };
-    auto issue_chunk = [&](Sym<NV> *d, uint32_t c) {  // layout A: wave w holds positions 16w + j
-      const uint32_t t = trunc_of(c);
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const uint32_t pos = 16 * w + j;
-        if (pos < t && !skipped(a, c * 64 + pos))
-          dev::load_sym_raw(d[j], src + (static_cast<uint64_t>(c) * 64 + pos) * sb, off, a.contig);
-        else dev::zero(d[j]);
-      }
-    };
-    Sym<NV> acc[16], nxt[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) dev::zero(acc[u]);
-    if constexpr (PF) issue_chunk(nxt, 0);
-    for (uint32_t c = 0; c < a.n_chunks; c++) {
-      const uint32_t t = trunc_of(c);
-      const RsTab *tc = a.tabs + c * TI;
-      asm volatile("" : "+s"(tc));  // opaque base: no per-group pointer IVs (SGPR spills)
-      Sym<NV> cur[16];
-      if constexpr (PF) {
-#pragma unroll
-        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
-      } else {
-        issue_chunk(cur, c);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; j++) dev::pair_halves(cur[j], a.contig);
-      if constexpr (PF) {
-        if (c + 1 < a.n_chunks) issue_chunk(nxt, c + 1);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; g++) {  // stage d=1, groups r = 16w + 4g
-        const uint32_t r = 16 * w + 4 * g;
-        if (r < t) ifft4(cur[4 * g], cur[4 * g + 1], cur[4 * g + 2], cur[4 * g + 3], tc + r / 4 * 3);
-      }
-      if (16 * w < t) {  // stage d=4, group r = 16w
-        if constexpr (SHARED) {
-          ifft4x4(cur, tc + 48 + w * 3);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 48 + w * 3);
-        }
-      }
-      __syncthreads();  // previous readers of lds are done
-#pragma unroll
-      for (int j = 0; j < 16; j++) lds_put(lds[16 * w + j], lane, cur[j]);
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < 16; u++) lds_get(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, cur[u]);  // layout B
-      if constexpr (SHARED) {
-        ifft4x4(cur, tc + 60);  // d=16
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++) ifft4(cur[i], cur[i + 4], cur[i + 8], cur[i + 12], tc + 60);  // d=16
-      }
-#pragma unroll
-      for (int u = 0; u < 16; u++) dev::xor_into(acc[u], cur[u]);  // root.zig:153-155
-    }
-    // FFT(0, 64, trunc m) on acc, root.zig:169
-    const RsTab *tf = a.tabs + a.n_chunks * TI;
-    if constexpr (SHARED) {
-      fft4x4(acc, tf);  // d=16 (layout B)
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf);  // d=16 (layout B)
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 16; u++) lds_put(lds[(u & 3) + 4 * w + 16 * (u >> 2)], lane, acc[u]);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 16; j++) lds_get(lds[16 * w + j], lane, acc[j]);  // layout A
-    if (16 * w < a.m) {  // d=4, group r = 16w
-      if constexpr (SHARED) {
-        fft4x4(acc, tf + 3 + w * 3);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++) fft4(acc[i], acc[i + 4], acc[i + 8], acc[i + 12], tf + 3 + w * 3);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < 4; g++) {  // d=1, groups r = 16w + 4g
-      const uint32_t r = 16 * w + 4 * g;
-      if (r < a.m) fft4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3], tf + 15 + r / 4 * 3);
-    }
-    uint8_t *dst = a.parity + s * a.parity_stripe_stride;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t pos = 16 * w + j;
-      if (pos < a.m) dev::store_sym(dst + pos * sb, off, acc[j], a.contig);
-    }
-  }
-}
-
 // ================================================= matrix reconstruct (e <= 8)
 // restored_j = XOR_i M_ij(in_i): the reconstruct of root.zig:268-335 is
 // GF(2)-linear in the received shards, so for one erasure pattern it is an
-// n_out x n_in matrix of 16x16 GF(2) maps (host-derived, rs_capi.cpp). Each
+// n_out x n_in matrix of 16x16 GF(2) maps (host-derived, rs_plans.cpp). Each
 // input is read once; its six bit-field selectors are shared by all n_out
 // multiply-accumulates. Reads k shards, writes e: the algorithmic minimum.
 template <int NV>
@@ -623,47 +513,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_matrix(DecodeArgs a) {
 // workgroup's 4 waves share the same 64 column units and split the e outputs,
 // EW per wave ("per-wave output-shard tiling"); each wave streams all k inputs
 // (the 4 waves read the same lines back to back: HBM once, L2 for the rest).
-template <int EW, int NV>
-__global__ __launch_bounds__(kBlock) void k_decode_mtile(DecodeArgs a) {
-  const uint64_t sb = a.shard_bytes;
-  if (blockIdx.x >= sb / 64 * (8 / NV) / 64) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t j0 = w * EW;
-  if (j0 >= a.n_out) return;  // no barriers in this kernel: idle waves may leave
-  const uint32_t off = dev::lane_byte_offset<NV>(blockIdx.x, lane, a.contig);
-  const uint64_t s = blockIdx.y;
-  typedef const __attribute__((address_space(4))) int32_t *CI;
-  const CI srcs = (CI)(a.pos_src);
-  const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
-  const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
-  const uint8_t *xs = a.xsrc + s * a.xsrc_stripe_stride;
-  const uint32_t stride = 4 * EW;  // padded outputs per table row
-  Sym<NV> acc[EW];
-#pragma unroll
-  for (int j = 0; j < EW; j++) dev::zero(acc[j]);
-  InFlight<NV> f;
-  issue_input(f, srcs[0], orig, rec, xs, sb, off, a.contig);
-  for (uint32_t i = 0; i < a.n_in; i++) {
-    Sym<NV> y;
-    take_input(y, f, a.contig);
-    if (i + 1 < a.n_in) issue_input(f, srcs[i + 1], orig, rec, xs, sb, off, a.contig);
-    Sel<NV> sel;
-    make_sel(sel, y);
-    const RsTab *row = a.tab_mat + static_cast<uint64_t>(i) * stride + j0;
-    asm volatile("" : "+s"(row));
-#pragma unroll
-    for (int j = 0; j < EW; j++) mac_sel(acc[j], sel, dev::load_tab(row + j));
-  }
-  uint8_t *out = a.out + s * a.out_stripe_stride;
-#pragma unroll
-  for (int j = 0; j < EW; j++)
-    if (j0 + j < a.n_out) dev::store_sym(out + static_cast<uint64_t>(j0 + j) * sb, off, acc[j], a.contig);
-}
-
-// Same product with VGPR tables: every v_perm_b32 then has only VGPR operands,
-// where SGPR tables cost one SGPR->VGPR v_mov per table pair (gfx9 VOP3 reads at
-// most one SGPR) — ~0.74 moves per v_perm in k_decode_mtile's ISA.
 template <int NV>
 __device__ __forceinline__ void mac_sel_v(Sym<NV> &x, const Sel<NV> &s, const uint32_t *lo, const uint32_t *hi) {
   using dev::perm;
@@ -1686,8 +1535,6 @@ static int fit_nv(int nv, uint64_t shard_bytes) {
   return nv;
 }
 
-static const char *env_variant() { return getenv("RS_AMD_VARIANT"); }
-
 static int env_nv(int dflt) {
   const char *e = getenv("RS_AMD_NV");
   if (!e) return dflt;
@@ -1724,7 +1571,7 @@ KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max
     const int nv = clamp_nv(fit_nv(std::min(env_nv(4), max_nv), shard_bytes), c, true);
     return {Variant::kRegister, c, nv, reg_name(true, c, nv)};
   }
-  if (C == 64 && shard_bytes % 512 == 0 && (env_variant() == nullptr || std::string(env_variant()) != "generic")) {
+  if (C == 64 && shard_bytes % 512 == 0) {
     int nv = std::min(std::min(env_nv(1), max_nv), 2);
     if (shard_bytes % (512 * nv)) nv = 1;  // whole 64-lane regions only
     return {Variant::kWaveSplit, 64, nv, nv == 1 ? "encode_ws64_nv1" : "encode_ws64_nv2"};
@@ -1809,8 +1656,7 @@ KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_
   const int nv = fit_nv(std::min(env_nv(4), max_nv), shard_bytes);
   const int ni = nv == 1 ? 0 : nv == 2 ? 1 : 2;
   KernelChoice kc{Variant::kMatrix, static_cast<int>(n_out), nv, kNames[n_out][ni]};
-  const char *pf = getenv("RS_AMD_PREFETCH");  // inputs in flight per lane (1, 2, 4)
-  kc.prefetch = pf ? atoi(pf) : 1;
+  kc.prefetch = 1;  // inputs in flight per lane (2 measured no faster)
   return kc;
 }
 
@@ -1899,28 +1745,11 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
     // one block per 64-lane region; 4 waves split the 64 positions
     const uint64_t regions = a.shard_bytes / 64 * (8 / kc.nv) / 64;
     const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
-    const char *ev = getenv("RS_AMD_WS64_SHARED");  // A/B switch: 1 (default) shared stage tables
-    const bool shared = !(ev && ev[0] == '0');
-    // A/B switch RS_AMD_WS64_LDS, default on: LDS-staged VGPR tables (no SGPR->VGPR
-    // moves, no SGPR spills). RS(200,55) 256 KiB x 256 after the load split: NV=1 7.36
-    // vs 7.62 ms, NV=2 9.34 vs 11.5 ms (profiles/r01/sweep_rs200_55_ws64_lds.jsonl;
-    // before the split, when every load was its own round trip, it measured slower)
-    const char *el = getenv("RS_AMD_WS64_LDS");
-    if (!(el && el[0] == '0')) {
-      if (kc.nv == 1) hipLaunchKernelGGL((k_encode_ws64l<1>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((k_encode_ws64l<2>), g, dim3(kBlock), 0, s, a);
-    } else {
-      // A/B switch RS_AMD_WS64_PF (next-chunk prefetch): default on for NV=2 only.
-      // RS(200,55) 256 KiB x 256: NV=1 7.57 (off) vs 7.92 ms (on, 87 -> 119 VGPRs);
-      // NV=2 14.6 vs 11.5 ms (profiles/r01/sweep_rs200_55_ws64_pf.jsonl)
-      const char *ep = getenv("RS_AMD_WS64_PF");
-      const bool pf = ep && ep[0] ? ep[0] == '1' : kc.nv == 2;
-#define RS_WS64(NV_, SH_, PF_) \
-  if (kc.nv == NV_ && shared == SH_ && pf == PF_) hipLaunchKernelGGL((k_encode_ws64<NV_, SH_, PF_>), g, dim3(kBlock), 0, s, a);
-      RS_WS64(1, true, true) RS_WS64(1, true, false) RS_WS64(1, false, true) RS_WS64(1, false, false)
-      RS_WS64(2, true, true) RS_WS64(2, true, false) RS_WS64(2, false, true) RS_WS64(2, false, false)
-#undef RS_WS64
-    }
+    // LDS-staged VGPR tables (no SGPR->VGPR moves, no SGPR spills): RS(200,55) 256 KiB x 256
+    // NV=1 7.36 vs 7.62 ms, NV=2 9.34 vs 11.5 ms against SGPR tables
+    // (profiles/r01/sweep_rs200_55_ws64_lds.jsonl)
+    if (kc.nv == 1) hipLaunchKernelGGL((k_encode_ws64l<1>), g, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_encode_ws64l<2>), g, dim3(kBlock), 0, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_encode_generic<1>, grid, dim3(kBlock), 0, s, a);
@@ -1941,15 +1770,9 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
   if (kc.variant == Variant::kMatrixTiled) {
     const uint64_t regions = a.shard_bytes / 64 * (8 / kc.nv) / 64;
     const dim3 g(static_cast<uint32_t>(regions), grid.y, 1);
-    const char *ev = getenv("RS_AMD_MTILE_LDS");  // A/B switch: 1 (default) LDS-staged VGPR tables
-    if (!(ev && ev[0] == '0')) {
-      if (kc.nv == 1) hipLaunchKernelGGL((k_decode_mtile_lds<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL((k_decode_mtile_lds<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
-    } else if (kc.nv == 1) {
-      hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
-    } else {
-      hipLaunchKernelGGL((k_decode_mtile<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
-    }
+    // LDS-staged VGPR tables: -13 % against SGPR tables at NV=1
+    if (kc.nv == 1) hipLaunchKernelGGL((k_decode_mtile_lds<kMtileEW, 1>), g, dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL((k_decode_mtile_lds<kMtileEW, 2>), g, dim3(kBlock), 0, s, a);
     return hipGetLastError();
   }
   if (kc.variant == Variant::kMatrix) {

@@ -421,7 +421,7 @@ int rs_fft_compile_check(uint64_t k, uint64_t m, uint32_t flags, double *compile
   return guarded([&]() -> int {
     int st = check_codec(k, m, fftnet::kUnitBytes);
     if (st) return st;
-    if (!fftnet::supports(k, m, fftnet::kUnitBytes)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes, true)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
     fftnet::Spec spec;
     spec.k = static_cast<uint32_t>(k);
     spec.m = static_cast<uint32_t>(m);
@@ -445,7 +445,7 @@ int rs_fft_selftest(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *skip,
   return guarded([&]() -> int {
     int st = check_codec(k, m, fftnet::kUnitBytes);
     if (st) return st;
-    if (!fftnet::supports(k, m, fftnet::kUnitBytes)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes, true)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
     fftnet::Spec spec;
     spec.k = static_cast<uint32_t>(k);
     spec.m = static_cast<uint32_t>(m);

@@ -19,14 +19,13 @@ bool supports(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 
 namespace {
 
-int env_int(const char *name, int def) {
-  const char *e = std::getenv(name);
-  return e && *e ? std::atoi(e) : def;
-}
 // code-shape knobs (part of the cache key): inputs loaded ahead, occupancy hint
-uint32_t prefetch() { return static_cast<uint32_t>(std::max(0, std::min(6, env_int("RS_AMD_PSYN_PF", 2)))); }
-int waves() { return std::max(0, std::min(8, env_int("RS_AMD_PSYN_WAVES", 3))); }
-bool skip_erased() { return env_int("RS_AMD_PSYN_SKIP", 1) != 0; }  // 3: 5.19 -> 5.07 ms (profiles/r02/patterns_psyn.jsonl)
+// code shape (measured, profiles/r02/patterns_psyn*.jsonl): inputs loaded 2 ahead, an
+// occupancy hint of 3 waves per SIMD, erased inputs skip their transform and network
+// (5.0-5.15 -> 4.67 ms on RS(10,4) 1 MiB x 2048)
+uint32_t prefetch() { return 2; }
+int waves() { return 3; }
+bool skip_erased() { return true; }
 
 std::string key_of(const Spec &s) {
   std::string k = "psyn2:p" + std::to_string(prefetch()) + "w" + std::to_string(waves()) + "s" +
@@ -151,7 +150,7 @@ std::string generate(const Spec &s, const std::string &name) {
   for (uint32_t i = 0; i < PF; i++) load(i);
   for (uint32_t i = 0; i < n_inputs; i++) {
     load(i + PF);
-    // RS_AMD_PSYN_SKIP: an erased input (read as zeros) skips its transform and network
+    // an erased input (read as zeros) skips its transform and network
     // under a wave-uniform branch; its load stays unconditional (prefetch order)
     if (skip_erased())
       o << "  if (!(" << (i < K ? "(em" + std::to_string(i / 32) + " >> " + std::to_string(i % 32) + ") & 1u"

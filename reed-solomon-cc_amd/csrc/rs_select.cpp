@@ -15,13 +15,9 @@ namespace host {
 // table register kernel — RS(40,12) 1 MiB 4.08 -> 2.95 ms, RS(100,6) 2.85 -> 2.35 ms,
 // RS(100,4) 2.49 -> 2.30 ms, RS(200,8) 2.75 -> 2.58 ms (profiles/r02/sweep_encode_async_net.jsonl).
 bool encode_net_async(uint64_t k, uint64_t m) {
-  const char *e = std::getenv("RS_AMD_NET_ASYNC_ENCODE");
-  if (e && *e && std::strcmp(e, "0") == 0) return false;
   const char *sh = std::getenv("RS_AMD_NET_SHARED");
   if (sh && *sh && std::strcmp(sh, "0") == 0) return false;
-  const char *lo = std::getenv("RS_AMD_NET_ASYNC_ENCODE_MIN_M");
-  const uint64_t m_min = lo && *lo ? static_cast<uint64_t>(std::atoi(lo)) : 1;
-  return m >= m_min && m <= jit::kMaxOut && !fftnet::supports(k, m, fftnet::kUnitBytes) &&
+  return m <= jit::kMaxOut && !fftnet::supports(k, m, fftnet::kUnitBytes) &&
          jit::supports_async(static_cast<uint32_t>(k), static_cast<uint32_t>(m), jit::kUnitBytes);
 }
 

@@ -186,7 +186,9 @@ def test_small_shard_net_kernels_compile_for_gfx950(monkeypatch, pieces):
 
 
 @pytest.mark.parametrize("k,m,flags", [(200, 55, 0), (200, 55, 3), (100, 20, 0), (64, 64, 1), (40, 50, 0),
-                                       (1000, 64, 0), (33, 17, 2)])
+                                       (1000, 64, 0), (33, 17, 2),
+                                       # chunk 16 (the per-stripe pattern path's syndromes)
+                                       (16, 16, 0), (40, 12, 3), (100, 16, 0), (9, 9, 0), (64, 10, 2)])
 def test_fft_kernel_arithmetic(k, m, flags):
     """The bit-sliced FFT encode kernel's schedule with its (u, v)-coordinate matrices
     (Cantor-basis subfield split) reproduces the codec's scalar encode, both quirk

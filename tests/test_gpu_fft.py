@@ -16,9 +16,7 @@ DEV = torch.device("cuda:0")
 
 SHAPES = [(200, 55), (100, 20), (64, 64), (32, 32), (40, 50), (300, 40), (128, 33), (33, 17), (256, 64),
           (1000, 64), (65, 64)]
-# chunk 16 (two waves per workgroup; RS_AMD_FFT_C16=1, off by default: no faster than
-# the networks / table kernels on the shapes measured, profiles/r02/sweep_fft_c16.jsonl)
-SHAPES_C16 = [(16, 16), (40, 12), (100, 16), (9, 9), (20, 9), (17, 16), (64, 10)]
+
 
 
 def enc(k, m, data, flags=0):
@@ -39,13 +37,6 @@ def test_fft_encode_vs_oracle(oracle, k, m, flags):
     got = enc(k, m, data, flags)
     exp = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
     assert np.array_equal(got, exp)
-
-
-@pytest.mark.parametrize("k,m", SHAPES_C16)
-@pytest.mark.parametrize("flags", [0, 3])
-def test_fft_encode_chunk16_vs_oracle(oracle, monkeypatch, k, m, flags):
-    monkeypatch.setenv("RS_AMD_FFT_C16", "1")
-    test_fft_encode_vs_oracle(oracle, k, m, flags)
 
 
 def test_fft_encode_strided(oracle):

@@ -28,7 +28,7 @@ for s in range(n):
 dp = torch.from_numpy(present).to(dev)
 out = torch.empty((n, max_e, sb), dtype=torch.uint8, device=dev)
 status = torch.empty((n,), dtype=torch.int32, device=dev)
-# extra variants: NAME=v1,v2 arguments after the stripe count (e.g. RS_AMD_PSYN_PF=1,2,3)
+# extra variants: NAME=v1,v2 arguments after the stripe count (e.g. RS_AMD_JIT=0,1)
 variants = [("RS_AMD_PATTERNS", p) for p in ("matrix", "auto", "fft", "matrix", "auto")]
 for arg in args:
     name, vals = arg.split("=")
