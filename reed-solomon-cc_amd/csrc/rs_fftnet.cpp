@@ -898,6 +898,8 @@ const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pendin
     if (!k) return nullptr;
     int local = 0;
     if (hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k->fn) != hipSuccess) local = 0;
+    // RS_AMD_FFT_ALLOW_SPILL=1: investigation hook (tools/spill_repro.py), run a spilled build
+    if (local && std::getenv("RS_AMD_FFT_ALLOW_SPILL")) return k;
     if (local == 0 || copy.prefetch == 0) {
       if (local) {
         err = "FFT kernel spills registers even without prefetch";
