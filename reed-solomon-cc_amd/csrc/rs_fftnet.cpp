@@ -232,7 +232,17 @@ __device__ __forceinline__ void tr8(u32 *x) {
 // raw buffer accesses: voffset = the lane's offset in the unit, soffset = the
 // (wave-uniform) shard offset; a resource with 0 records reads zeros
 #define LDB(r, vo, so) __builtin_amdgcn_raw_buffer_load_b128((r), (vo), (so), RS_AUX_LD)
-#define STB(v, r, vo, so) __builtin_amdgcn_raw_buffer_store_b128((v), (r), (vo), (so), RS_AUX_ST)
+// A 128-bit store's data registers must not be rewritten by the next instruction: LLVM
+// inserts that wait state for buffer stores only when soffset is not a register, and a
+// build whose next VALU overwrote the first data dword stored that value in lanes 12-15
+// of every row (profiles/r03/spill_root_cause.md). The s_nop reads the data, so the
+// registers stay live until it has issued: at least one wait state, whatever the schedule.
+#define STB(v, r, vo, so)                                                      \
+  {                                                                            \
+    const v4 sv_ = (v);                                                        \
+    __builtin_amdgcn_raw_buffer_store_b128(sv_, (r), (vo), (so), RS_AUX_ST);   \
+    asm volatile("s_nop 0" ::"v"(sv_) : "memory");                             \
+  }
 // 2 KiB slice of a shard: lanes 0-31 read the lo halves, 32-63 the hi halves of
 // 16 chunks per KiB; one v_permlane32_swap per dword pairs them; then an 8x8 bit
 // transpose per byte lane: P[j] = (lo plane j | hi plane j) per byte (nibbles)
@@ -898,7 +908,7 @@ const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pendin
     if (!k) return nullptr;
     int local = 0;
     if (hipFuncGetAttribute(&local, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, k->fn) != hipSuccess) local = 0;
-    // RS_AMD_FFT_ALLOW_SPILL=1: investigation hook (tools/spill_repro.py), run a spilled build
+    // RS_AMD_FFT_ALLOW_SPILL=1: run a spilled build (tools/spill_repro.py, spill_root_cause.md)
     if (local && std::getenv("RS_AMD_FFT_ALLOW_SPILL")) return k;
     if (local == 0 || copy.prefetch == 0) {
       if (local) {

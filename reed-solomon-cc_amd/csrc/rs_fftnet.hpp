@@ -74,8 +74,9 @@ std::string cache_key(const Spec &s);
 std::string kernel_name(const Spec &s);
 
 // compiled kernel (cached per device and spec); async: background compile (see jit::get_source).
-// A build whose registers spill to scratch is rebuilt with less prefetch (spill-free
-// code only: scratch spills of these kernels measured unreliable on gfx950).
+// A build whose registers spill to scratch is rebuilt with less prefetch (spills cost more
+// than the prefetch gains). The wrong bytes of round 2's spilled builds were a store-data
+// hazard, now closed for every build (profiles/r03/spill_root_cause.md, STB).
 const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pending);
 bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_bytes);
 

@@ -42,9 +42,34 @@ for r in range(reps):
     diff = got != exp
     if diff.any():
         st_, sh_, by_ = np.nonzero(diff)
+        # per bad 1 KiB block (stripe, shard, block): bad bytes, and whether the block
+        # reads as the fill value (store missing) or as other bytes (wrong data)
+        blocks = {}
+        for a, b_, c in zip(st_.tolist(), sh_.tolist(), (by_ // 1024).tolist()):
+            blocks[(a, b_, c)] = blocks.get((a, b_, c), 0) + 1
+        kinds = {}
+        for (a, b_, c), cnt in blocks.items():
+            g = got[a, b_, c * 1024:(c + 1) * 1024]
+            kind = "zero" if not g.any() else "other"
+            if kind == "other":  # the right bytes of another stripe / shard / block?
+                for a2 in range(n):
+                    for b2 in range(m):
+                        for c2 in range(sb // 1024):
+                            if (a2, b2, c2) != (a, b_, c) and np.array_equal(g, exp[a2, b2, c2 * 1024:(c2 + 1) * 1024]):
+                                kind = "copy_of:%d/%d/%d" % (a2, b2, c2)
+                                break
+                        if kind != "other":
+                            break
+                    if kind != "other":
+                        break
+            offs = np.nonzero(diff[a, b_, c * 1024:(c + 1) * 1024])[0]
+            xr = (got[a, b_, c * 1024:(c + 1) * 1024] ^ exp[a, b_, c * 1024:(c + 1) * 1024])[offs]
+            kinds.setdefault(kind.split(":")[0], []).append([a, b_, c, cnt] + ([kind] if ":" in kind else []) +
+                                                           [offs.tolist()[:64], xr.tolist()[:16]])
         bad_launches.append({"rep": r, "bytes": int(diff.sum()), "stripes": sorted(set(st_.tolist()))[:8],
                              "shards": sorted(set(sh_.tolist()))[:8], "first_byte": int(by_.min()),
-                             "units_2k": sorted(set((by_ // 2048).tolist()))[:8]})
+                             "blocks_1k": len(blocks), "block_offsets": sorted(set(c for (_, _, c) in blocks)),
+                             "kinds": {k: v[:3] for k, v in kinds.items()}})
 print(json.dumps({"prefetch": os.environ.get("RS_AMD_FFT_PREFETCH"), "allow_spill": os.environ.get("RS_AMD_FFT_ALLOW_SPILL"),
                   "stack": stack, "kernel": R.encode_kernel_name(k, m, sb), "reps": reps,
                   "bad_launches": len(bad_launches), "detail": bad_launches[:6]}), flush=True)
