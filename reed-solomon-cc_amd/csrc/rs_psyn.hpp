@@ -17,7 +17,7 @@
 // coordinates through one fixed 16 x 16 network each.
 //
 // This replaces the per-stripe e x k table matrices of the matrix path (40 table
-// multiplies per column for RS(10,4), v_perm-bound) for codes with k <= 64 and
+// multiplies per column for RS(10,4), v_perm-bound) for codes with k <= kMaxK and
 // m <= kMaxM; the reference evaluates the erasure locator per call
 // (Generic.zig:200-215, root.zig:268-335).
 #pragma once
