@@ -84,3 +84,43 @@ def test_random_code_vs_oracle(oracle, seed):
         assert st[s] == 0, (s, st[s], path)
         assert np.array_equal(got[s, :len(miss[s])], data[s, miss[s]]), (k, m, sb, s, miss[s], path)
         assert (got[s, len(miss[s]):] == 0xAB).all(), (s, path)
+
+
+def draw_low(seed):
+    """A low-rate code (round 3: any (k, m) useHighRate rejects), shard size, stripes."""
+    rng = np.random.default_rng(seed)
+    while True:
+        k = int(rng.choice([int(rng.integers(1, 17)), int(rng.integers(17, 80)), int(rng.integers(80, 300))]))
+        m = int(rng.choice([int(rng.integers(k, 2 * k + 2)), int(rng.integers(k, 700)), int(rng.integers(k, 2500))]))
+        if m >= 1 and R.use_high_rate(k, m) == 0:
+            break
+    sb = int(rng.choice(SHARD_SIZES[:5]))  # the oracle's low-rate encode is scalar: modest sizes
+    n = int(rng.integers(1, 4))
+    return rng, k, m, sb, n
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_low_rate_code(oracle, seed):
+    """Random low-rate codes (parity unpinned: the oracle restates the same published
+    algorithm), 64 B - 4 KiB shards: encode vs the oracle, then one
+    erasure pattern of up to min(k, m) lost shards restored from the rest."""
+    rng, k, m, sb, n = draw_low(5000 + seed)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    d = torch.from_numpy(data).to(DEV)
+    p = torch.zeros((n, m, sb), dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p)
+    torch.cuda.synchronize()
+    par = p.cpu().numpy()
+    for s in range(n):
+        st, exp = oracle.encode_low(k, m, data[s])
+        assert st == 0 and np.array_equal(par[s], exp), (k, m, sb, n, s, R.encode_kernel_name(k, m, sb))
+    lost = rng.choice(k + m, size=int(rng.integers(1, min(k, m) + 1)), replace=False)
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    missing = [i for i in range(k) if not present[i]]
+    if missing:
+        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8, device=DEV)
+        R.reconstruct_batch_dev(k, m, present.tolist(), d, p, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), data[:, missing]), \
+            (k, m, sb, n, missing, R.reconstruct_kernel_name(k, m, sb, present.tolist()))
