@@ -233,6 +233,19 @@ int rs_fft_compile_check(uint64_t original_count, uint64_t recovery_count, uint3
 int rs_fft_selftest(uint64_t original_count, uint64_t recovery_count, uint32_t flags, const uint8_t *skip,
                     int trials, uint64_t *mismatches);
 
+/* Fused FFT reconstruct of wide codes (replaces the reference's
+ * Decoder.decode, root.zig:268-335, for chunk 16 / 32 / 64 codes, corrected multiply):
+ * the syndromes of e recovery rows and the erasure-locator decode in one kernel, the
+ * pattern as data. rs_fft_decode_compile_check generates and compiles it (no device);
+ * rs_fft_decode_selftest runs its schedule on scalar symbols (host) for `trials` random
+ * stripes losing e originals (and random surplus recovery shards) against the data:
+ * *mismatches = wrong restored symbols. RS_ERR_INVALID_ARGUMENT if the code has no such
+ * kernel or e > recovery_count. */
+int rs_fft_decode_compile_check(uint64_t original_count, uint64_t recovery_count, double *compile_ms,
+                                uint64_t *code_bytes);
+int rs_fft_decode_selftest(uint64_t original_count, uint64_t recovery_count, uint32_t erased, int trials,
+                           uint64_t *mismatches);
+
 /* Host check of the low-rate reconstruct's algebra (no device): `trials` random stripes
  * of one symbol per shard, encoded by the low-rate encode, lose 1..min(k, m) random
  * originals plus random recovery shards (>= k present), and are restored by the

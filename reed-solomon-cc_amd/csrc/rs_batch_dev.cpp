@@ -223,6 +223,26 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
         return RS_OK;
       }
     }
+    // the fused FFT reconstruct (wide codes): syndromes and decode in one kernel, the
+    // pattern as data. RS_AMD_FDEC=auto runs it until a network compiled
+    // for the pattern is loaded (as fast for the syndrome maps, faster for few losses)
+    if (plan->fdec_blk && max_nv == 4) {
+      const jit::Kernel *nk = plan->net && fdec_mode() != 1 ? net_kernel(*plan->net, sb) : nullptr;
+      if (!nk) {
+        std::shared_ptr<WpsSlot> ws;
+        wps_slot(dev, k, m, 0, ws);
+        const fftnet::Spec *dfs = nullptr;
+        if (const jit::Kernel *fk = fft_kernel(*ws->dec, sb, &dfs)) {
+          HIP_TRY(fftnet::launch(*fk, *dfs, static_cast<const uint8_t *>(d_original ? d_original : d_recovery),
+                                 orig_stride, static_cast<const uint8_t *>(d_recovery), rec_stride,
+                                 static_cast<uint8_t *>(d_restored), out_stride, sb, n_stripes,
+                                 static_cast<hipStream_t>(stream), static_cast<const uint32_t *>(plan->fdec_blk->p),
+                                 plan->fdec_words, true));
+          return RS_OK;
+        }
+        if (fdec_mode() == 1) return fail(RS_ERR_DEVICE, "RS_AMD_FDEC=1: fused FFT reconstruct kernel unavailable");
+      }
+    }
     if (plan->net && !plan->syndrome && max_nv == 4) {
       if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,

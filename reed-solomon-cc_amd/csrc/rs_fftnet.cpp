@@ -277,6 +277,26 @@ __device__ __forceinline__ void unplanes2(u32 *P, v4 &a, v4 &b) {
     __builtin_amdgcn_s_barrier();                                  \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); \
   }
+// Spec::decode: multiplication by a uniform runtime scalar from its 128 nibble masks
+// (scalar_masks), read through the constant address space (scalar loads):
+// out_i = XOR_j (x_j & M[16 i + j]) ^ (SWN(x_j) & M[16 i + 8 + j])
+typedef const __attribute__((address_space(4))) u32 *cptr;
+__device__ __forceinline__ void rmul(u32 *x, cptr M) {
+  u32 s[8], o[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) s[j] = SWN(x[j]);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u32 a = x[0] & M[16 * i];
+#pragma unroll
+    for (int j = 1; j < 8; j++) a = __builtin_amdgcn_bitop3_b32(a, x[j], M[16 * i + j], 0x78);
+#pragma unroll
+    for (int j = 0; j < 8; j++) a = __builtin_amdgcn_bitop3_b32(a, s[j], M[16 * i + 8 + j], 0x78);
+    o[i] = a;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = o[i];
+}
 )HIP";
 
 int env_int(const char *name, int def) {
@@ -286,7 +306,10 @@ int env_int(const char *name, int def) {
 
 
 int prefetch_of(const Spec &s) {
-  return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", 4)));
+  // the decode tail keeps the IFFT result live across its blocks: no register room for
+  // the next unit's loads (prefetch 2 spills, 0 does not: 241 VGPRs for RS(200,55))
+  const int def = s.decode ? 0 : 4;
+  return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", def)));
 }
 
 struct Gen {
@@ -520,7 +543,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   if (!g.st) g.st = &dummy;
   std::ostringstream &o = g.o;
   const uint32_t NW = P.NW, C = P.C;
-  bool any_xor = false;
+  bool any_xor = s.decode;  // the decode reads the recovery rows R
   for (uint32_t q = 0; q < s.m; q++) any_xor |= P.out_mode[q] == kOutXorRec;
   // non-temporal loads and stores (cache policy bit nt = 2): RS(200,55) 256 KiB encode
   // 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
@@ -580,6 +603,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   rsrc_pair(hdr2, "RD", "data", "ds", "stripe", s.k, "");
   rsrc_pair(hdr2, "RO", "out", "os", "stripe", s.m, "");
   if (dyn) hdr2 << "  const u32 *DM = dm + stripe * dmw;\n";
+  if (s.decode) hdr2 << "  const cptr DMc = (cptr)DM;\n";
   if (any_xor) rsrc_pair(hdr2, "RR", "rec", "rs", "stripe", s.m, "");
   hdr2 << "  u32 ";
   for (uint32_t r = 0; r < 8; r++)
@@ -811,6 +835,13 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         g.butterfly(wname(rx), z[rx], wname(ry), z[ry], false, P.get_tw(b.log_m));
       }
     }
+    if (s.decode) {  // Enc(d') rows p < m stay in registers for the decode tail
+      for (uint32_t r = 0; r < 8; r++)
+        if (P.posA(w, r) < s.m && z[r])
+          for (int i = 0; i < 8; i++) o << "  " << wname(r) << "_" << i << " = 0u;\n";
+      o << "  }\n";
+      continue;
+    }
     // basis change back, planes -> bytes, store (or rec ^ parity)
     g.ops = &g.st->ops_io;
     if (dyn)  // rows this stripe stores: one byte of its store mask
@@ -836,6 +867,175 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     }
     g.ops = &g.st->ops_a;
     o << "  }\n";
+  }
+  if (s.decode) {
+    // ---- decode tail (Spec::decode): w_p = L_p (rec_p ^ Enc_p) for the
+    // rows R (layout A), a = IFFT(size C, trunc m, skew 0) (A then B), and per data block K
+    // with an erasure: FFT(a, size C, trunc t_K, skew KC) (B then A), x_g = (L'_g beta_K) y_q
+    const uint32_t dwm = dyn_store_word(P) + 2, mko = decode_mask_offset(s);
+    g.ops = &g.st->ops_io;
+    o << "  {  // syndromes of the rows R times the locator (one code path, runtime scalars)\n"
+      << "  const u32 ub0 = DMc[" << dwm + 1 << "], ub1 = DMc[" << dwm + 2 << "];\n";
+    for (uint32_t r = 0; r < 8; r++)
+      o << "  const u32 pd" << r << " = w * 8u + " << r << "u;\n  const bool us" << r << " = ((pd" << r
+        << " < 32u ? ub0 >> pd" << r << " : ub1 >> (pd" << r << " - 32u)) & 1u) != 0u;\n  const v4 ra" << r
+        << " = LDB(us" << r << " ? RR : RZ, uo, pd" << r << " * sbl), rb" << r << " = LDB(us" << r
+        << " ? RR1 : RZ, uo1, pd" << r << " * sbl);\n";
+    for (uint32_t r = 0; r < 8; r++) {
+      const auto W = Gen::regs(wname(r));
+      o << "  if (us" << r << ") {\n  u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q);\n";
+      std::vector<std::string> q(8);
+      for (int i = 0; i < 8; i++) q[i] = "Q[" + std::to_string(i) + "]";
+      g.basis_change(q);
+      o << "  u32 X[8] = {";
+      for (int i = 0; i < 8; i++) o << W[i] << " ^ Q[" << i << "]" << (i < 7 ? ", " : "};\n");
+      o << "  rmul(X, (cptr)(DM + " << mko << "u + pd" << r << " * 128u));\n";
+      for (int i = 0; i < 8; i++) o << "  " << W[i] << " = X[" << i << "];\n";
+      o << "  } else {\n";
+      for (int i = 0; i < 8; i++) o << "  " << W[i] << " = 0u;\n";
+      o << "  }\n";
+    }
+    o << "  }\n";
+    // IFFT(size C, trunc m, skew 0): A layers per wave, A -> B, B layers
+    const std::vector<Layer> il = ifft_layers(C, s.m, 0);
+    std::vector<std::vector<uint8_t>> zA(NW, std::vector<uint8_t>(8, 0));
+    std::vector<uint8_t> liveB(8, 0);
+    for (uint32_t w = 0; w < NW; w++) {
+      bool z[8];
+      for (uint32_t r = 0; r < 8; r++) z[r] = P.posA(w, r) >= s.m;
+      for (const Layer &L : il) {
+        if (!P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf)
+          if (P.waveA(b.x) == w && !(z[P.regA(b.x)] && z[P.regA(b.y)])) z[P.regA(b.x)] = z[P.regA(b.y)] = false;
+      }
+      for (uint32_t r = 0; r < 8; r++) {
+        zA[w][r] = z[r];
+        if (!z[r]) liveB[P.regB(P.posA(w, r))] = 1;
+      }
+    }
+    g.ops = &g.st->ops_a;
+    o << "  {\n  LQ();\n";
+    for (uint32_t w = 0; w < NW; w++) {
+      bool z[8];
+      for (uint32_t r = 0; r < 8; r++) z[r] = P.posA(w, r) >= s.m;
+      o << "  " << (w ? "else if" : "if") << " (w == " << w << "u) {\n";
+      for (const Layer &L : il) {
+        if (!P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf) {
+          if (P.waveA(b.x) != w) continue;
+          const uint32_t rx = P.regA(b.x), ry = P.regA(b.y);
+          g.butterfly(wname(rx), z[rx], wname(ry), z[ry], true, P.get_tw(b.log_m));
+        }
+      }
+      for (uint32_t r = 0; r < 8; r++) {
+        const uint32_t p = P.posA(w, r), t = P.regB(p);
+        if (!liveB[t]) continue;
+        std::vector<std::string> v = Gen::regs(wname(r));
+        if (z[r]) v.assign(8, "0u");
+        lds_write("0", P.waveB(p) * 8 + t, v);
+      }
+      o << "  }\n";
+    }
+    o << "  BAR();\n";
+    bool za[8];
+    for (uint32_t t = 0; t < 8; t++) {
+      za[t] = !liveB[t];
+      if (liveB[t]) lds_read("(w * 8u)", t, Gen::regs(cname(t)));
+    }
+    o << "  BAR();\n  }\n";
+    g.ops = &g.st->ops_b;
+    for (const Layer &L : il) {
+      if (P.inA(L.bit)) continue;
+      for (const Bf &b : L.bf) {
+        if (P.waveB(b.x) != 0) continue;
+        const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+        g.butterfly(cname(tx), za[tx], cname(ty), za[ty], true, P.get_tw(b.log_m));
+      }
+    }
+    for (uint32_t t = 0; t < 8; t++)
+      if (!za[t]) g.pin(Gen::regs(cname(t)));
+    // per data block K: FFT(size C, trunc t_K, skew KC) of a
+    const uint32_t nblk = (s.k + C - 1) / C;
+    for (uint32_t K = 1; K <= nblk; K++) {
+      const uint32_t tK = std::min<uint32_t>(C, s.k - (K - 1) * C);
+      const std::vector<Layer> fl = fft_layers(C, tK, static_cast<uint64_t>(K) * C);
+      std::vector<uint8_t> nd(C, 0);
+      for (uint32_t q = 0; q < tK; q++) nd[q] = 1;
+      for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
+        if (!P.inA(it->bit)) continue;
+        for (const Bf &b : it->bf)
+          if (nd[b.x] || nd[b.y]) nd[b.x] = nd[b.y] = 1;
+      }
+      o << "  __builtin_amdgcn_sched_barrier(0);\n  if ((DMc[" << dwm << "] >> " << K << "u) & 1u) {  // data block " << K
+        << ": FFT(size " << C << ", trunc " << tK << ", skew_delta " << K * C << ")\n";
+      g.ops = &g.st->ops_b;
+      bool zb[8];
+      for (uint32_t t = 0; t < 8; t++) {
+        zb[t] = za[t];
+        if (!za[t]) g.copy(Gen::regs(bname(t)), Gen::regs(cname(t)));
+      }
+      for (const Layer &L : fl) {
+        if (P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf) {
+          if (P.waveB(b.x) != 0) continue;
+          const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+          g.butterfly(bname(tx), zb[tx], bname(ty), zb[ty], false, P.get_tw(b.log_m));
+        }
+      }
+      std::vector<uint8_t> nB(8, 0), rA(8, 0);
+      for (uint32_t q = 0; q < C; q++)
+        if (nd[q]) {
+          nB[P.regB(q)] = 1;
+          if (!zb[P.regB(q)]) rA[P.regA(q)] = 1;
+        }
+      o << "  {\n  LQ();\n";
+      for (uint32_t t = 0; t < 8; t++)
+        if (nB[t] && !zb[t]) lds_write("w", t << P.WB, Gen::regs(bname(t)));
+      o << "  BAR();\n";
+      for (uint32_t r = 0; r < 8; r++)
+        if (rA[r]) lds_read("(w * 8u)", r, Gen::regs(wname(r)));
+      o << "  BAR();\n  }\n";
+      g.ops = &g.st->ops_a;
+      bool firstw = true;
+      for (uint32_t w = 0; w < NW; w++) {
+        if (P.posA(w, 0) >= tK) continue;
+        o << "  " << (firstw ? "if" : "else if") << " (w == " << w << "u) {\n";
+        firstw = false;
+        bool z[8];
+        for (uint32_t r = 0; r < 8; r++) {
+          const uint32_t p = P.posA(w, r);
+          z[r] = zb[P.regB(p)] || !nd[p];
+        }
+        for (const Layer &L : fl) {
+          if (!P.inA(L.bit)) continue;
+          for (const Bf &b : L.bf) {
+            if (P.waveA(b.x) != w) continue;
+            const uint32_t rx = P.regA(b.x), ry = P.regA(b.y);
+            g.butterfly(wname(rx), z[rx], wname(ry), z[ry], false, P.get_tw(b.log_m));
+          }
+        }
+        for (uint32_t r = 0; r < 8; r++)
+          if (P.posA(w, r) < tK && z[r])
+            for (int i = 0; i < 8; i++) o << "  " << wname(r) << "_" << i << " = 0u;\n";
+        o << "  }\n";
+      }
+      // erased shards of the block: x_g = (L'_g beta_K) y_q, one code path for all waves
+      g.ops = &g.st->ops_io;
+      for (uint32_t r = 0; r < 8; r++) {
+        const auto W = Gen::regs(wname(r));
+        const uint32_t g0 = (K - 1) * C;
+        o << "  { const u32 q = w * 8u + " << r << "u;\n  const u32 row = q < " << tK << "u ? DMc[" << dwm + 3 + g0
+          << "u + q] : 0xFFFFFFFFu;\n  if (row != 0xFFFFFFFFu) {\n  u32 X[8] = {";
+        for (int i = 0; i < 8; i++) o << W[i] << (i < 7 ? ", " : "};\n");
+        o << "  rmul(X, (cptr)(DM + " << mko + 128 * (s.m + g0) << "u + q * 128u));\n";
+        std::vector<std::string> xs(8);
+        for (int i = 0; i < 8; i++) xs[i] = "X[" + std::to_string(i) + "]";
+        g.basis_change(xs);
+        o << "  v4 a, b; unplanes2(X, a, b);\n  const u32 so = row * sbl;\n  STB(a, RO, uo, so); STB(b, RO1, uo1, so);\n"
+          << "  }\n  }\n";
+      }
+      o << "  }\n";
+    }
   }
   o << "  stripe = stripe_n; uu = uu_n;\n";
   o << "  }\n}\n";
@@ -872,7 +1072,7 @@ std::string cache_key(const Spec &s) {
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
-                  (s.dyn ? "dyn:" : "");
+                  (s.dyn ? "dyn:" : "") + (s.decode ? "dec:" : "");
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
   k.push_back(':');
   for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));
@@ -883,7 +1083,8 @@ std::string kernel_name(const Spec &s) {
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : cache_key(s)) h = (h ^ c) * 1099511628211ull;
   char name[96];
-  std::snprintf(name, sizeof name, "rs_fft_%s_k%u_m%u_%016llx", s.inverse ? "inverse" : "encode", s.k, s.m,
+  std::snprintf(name, sizeof name, "rs_fft_%s_k%u_m%u_%016llx",
+                s.inverse ? "inverse" : s.decode ? "decode" : "encode", s.k, s.m,
                 static_cast<unsigned long long>(h));
   return name;
 }
@@ -891,6 +1092,111 @@ std::string kernel_name(const Spec &s) {
 std::string generate(const Spec &s, const std::string &name) { return gen_source(s, name, nullptr); }
 
 uint32_t dyn_mask_words(const Spec &s) { return dyn_store_word(make_plan(s)) + 2; }
+
+uint32_t decode_mask_offset(const Spec &s) { return (dyn_mask_words(s) + 3 + s.k + 15) & ~15u; }
+uint32_t decode_block_words(const Spec &s) { return decode_mask_offset(s) + (s.m + s.k) * 128; }
+
+namespace {
+uint16_t gmul(uint16_t x, uint16_t y) { return x && y ? mul16(x, tables().log[y]) : 0; }
+uint16_t tw_elem(uint64_t idx) {  // the element a butterfly multiplies by (0: XOR-only)
+  const uint16_t l = sk(idx);
+  return l == kModulus ? 0 : tables().exp[l];
+}
+}  // namespace
+
+// The decode transform of root.zig:268-335 (W = ceilPow2(C + k) points) on a residual
+// codeword that is zero outside positions [0, C): the IFFT's layers of distance >= C
+// spread block 0 into every block as scalar multiples lambda_K of a = IFFT_C(block 0),
+// the formal derivative adds lambda of the neighbouring blocks (its in-block part keeps
+// the form lambda_K D_C(a)), and the FFT's layers of distance >= C combine blocks
+// again. Tracking each block as alpha_K D_C(a) + beta_K a gives alpha_K = 0 for every
+// data block, so block K's evaluations are beta_K FFT_{C, skew KC}(a).
+bool decode_betas(uint32_t k, uint32_t m, std::vector<uint16_t> &beta) {
+  const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k), nb = W / C;
+  std::vector<uint16_t> lam(nb, 0), al(nb, 0), be(nb, 0);
+  lam[0] = 1;
+  for (uint64_t d = C; d < W; d *= 2)  // ifftPartial: y ^= x; x ^= t y (Generic.zig:171-192)
+    for (uint64_t g = 0; g < W; g += 2 * d) {
+      const uint16_t t = tw_elem(g + d - 1);
+      for (uint64_t i = g; i < g + d; i += C) {
+        const uint64_t x = i / C, y = (i + d) / C;
+        lam[y] ^= lam[x];
+        lam[x] ^= gmul(t, lam[y]);
+      }
+    }
+  for (uint64_t K = 0; K < nb; K++) {  // root.zig:309-315: block K ^= raw block K | bit
+    al[K] = lam[K];
+    for (uint64_t b = 1; b < nb; b <<= 1)
+      if (!(K & b)) be[K] ^= lam[K | b];
+  }
+  for (uint64_t d = W / 2; d >= C; d /= 2)  // fftPartial: x ^= t y; y ^= x (Generic.zig:149-169)
+    for (uint64_t g = 0; g < W; g += 2 * d) {
+      const uint16_t t = tw_elem(g + d - 1);
+      for (uint64_t i = g; i < g + d; i += C) {
+        const uint64_t x = i / C, y = (i + d) / C;
+        al[x] ^= gmul(t, al[y]);
+        be[x] ^= gmul(t, be[y]);
+        al[y] ^= al[x];
+        be[y] ^= be[x];
+      }
+    }
+  beta = be;
+  for (uint64_t K = 1; K < nb; K++)
+    if (al[K]) return false;
+  return true;
+}
+
+void uv_basis(uint32_t p[8]) {
+  for (int i = 0; i < 8; i++) p[i] = basis().p[i];
+}
+
+void scalar_masks(uint16_t c, uint32_t *M) {
+  std::memset(M, 0, 128 * sizeof(uint32_t));
+  if (!c) return;
+  const Tw t = twiddle(tables().log[c], false);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) {
+      M[16 * i + j] = ((t.A[i] >> j & 1) ? 0x0F0F0F0Fu : 0u) | ((t.D[i] >> j & 1) ? 0xF0F0F0F0u : 0u);
+      M[16 * i + 8 + j] = ((t.B[i] >> j & 1) ? 0x0F0F0F0Fu : 0u) | ((t.Cm[i] >> j & 1) ? 0xF0F0F0F0u : 0u);
+    }
+}
+
+int decode_block(const Spec &s, const uint8_t *present, uint32_t *blk) {
+  const uint32_t k = s.k, m = s.m, C = static_cast<uint32_t>(ceil_pow2(m));
+  const uint32_t dwm = dyn_mask_words(s), mko = decode_mask_offset(s);
+  std::memset(blk, 0, decode_block_words(s) * sizeof(uint32_t));
+  std::vector<uint16_t> beta;
+  if (!decode_betas(k, m, beta)) return RS_ERR_INVALID_ARGUMENT;
+  uint32_t e = 0;
+  for (uint32_t g = 0; g < k; g++) e += present[g] ? 0 : 1;
+  std::vector<uint8_t> received(ceil_pow2(C + k), 0);
+  uint32_t nr = 0;
+  for (uint32_t p = 0; p < m && nr < e; p++)
+    if (present[k + p]) {
+      received[p] = 1;
+      blk[dwm + 1 + p / 32] |= 1u << (p % 32);
+      nr++;
+    }
+  if (nr < e) return RS_ERR_NOT_ENOUGH_SHARDS;
+  uint32_t row = 0;
+  for (uint32_t g = 0; g < k; g++) {
+    received[C + g] = present[g] ? 1 : 0;
+    blk[dwm + 3 + g] = present[g] ? 0xFFFFFFFFu : row++;
+    if (!present[g]) {
+      blk[g / 32] |= 1u << (g % 32);
+      blk[dwm] |= 1u << ((C + g) / C);
+    }
+  }
+  std::vector<uint16_t> er(kOrder);
+  erasure_logs(received.data(), k, m, er.data());  // root.zig:277-289 (rows off R count as erased)
+  const Tables &T = tables();
+  for (uint32_t p = 0; p < m; p++)
+    if (received[p]) scalar_masks(T.exp[er[p]], blk + mko + 128 * p);  // root.zig:292-295
+  for (uint32_t g = 0; g < k; g++)
+    if (!present[g])  // root.zig:321-326, with the block's beta
+      scalar_masks(gmul(beta[(C + g) / C], T.exp[kModulus - er[C + g]]), blk + mko + 128 * (m + g));
+  return RS_OK;
+}
 
 Stats stats(const Spec &s) {
   Stats st;
@@ -911,7 +1217,10 @@ const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pendin
     // RS_AMD_FFT_ALLOW_SPILL=1: run a spilled build (tools/spill_repro.py, spill_root_cause.md)
     if (local && std::getenv("RS_AMD_FFT_ALLOW_SPILL")) return k;
     if (local == 0 || copy.prefetch == 0) {
-      if (local) {
+      // a decode kernel of a long code (RS(1000,64): 16 blocks) may keep a few registers
+      // in scratch even without prefetch; since the store-data hazard fix such builds are
+      // bit-exact (spill_root_cause.md), and they beat every other reconstruct form there
+      if (local && !copy.decode) {
         err = "FFT kernel spills registers even without prefetch";
         return nullptr;
       }
@@ -939,7 +1248,9 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
   if (n_stripes == 0) return hipSuccess;
   if (!supports(s.k, s.m, sb, s.dyn) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
     return hipErrorInvalidValue;
-  if (s.dyn && (s.pieces != 1 || !dmask || dmask_words < dyn_mask_words(s))) return hipErrorInvalidValue;
+  if (s.dyn && (s.pieces != 1 || !dmask || dmask_words < (s.decode ? decode_block_words(s) : dyn_mask_words(s))))
+    return hipErrorInvalidValue;
+  if (s.decode && (!s.dyn || s.inverse || s.flags || !rec)) return hipErrorInvalidValue;
   const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));
   static std::mutex mu;
   static std::map<int, int> cus;
@@ -1024,6 +1335,90 @@ uint64_t selftest(const Spec &s, int trials) {
       continue;
     }
     for (uint32_t q = 0; q < s.m; q++) bad += to_uv(acc[q]) != ref[q];
+  }
+  return bad;
+}
+
+uint64_t decode_selftest(uint32_t k, uint32_t m, uint32_t e, int trials) {
+  Spec s;
+  s.k = k;
+  s.m = m;
+  s.dyn = s.decode = true;
+  Plan P = make_plan(s);
+  const uint32_t C = P.C, dwm = dyn_mask_words(s), mko = decode_mask_offset(s);
+  std::mt19937_64 rng(777 + k * 131 + m * 7 + e);
+  uint64_t bad = 0;
+  auto apply = [&](std::vector<uint16_t> &v, const Layer &L) {  // the kernel's butterflies in (u|v) coordinates
+    for (const Bf &b : L.bf) {
+      const Tw &t = P.get_tw(b.log_m);
+      auto mulv = [&](uint16_t y) -> uint16_t {
+        if (t.zero) return 0;
+        uint16_t r = 0;
+        for (int i = 0; i < 8; i++) {
+          const uint8_t u = y & 0xFF, vv = y >> 8;
+          r |= static_cast<uint16_t>(((__builtin_popcount(t.A[i] & u) ^ __builtin_popcount(t.B[i] & vv)) & 1) << i);
+          r |= static_cast<uint16_t>(((__builtin_popcount(t.Cm[i] & u) ^ __builtin_popcount(t.D[i] & vv)) & 1) << (8 + i));
+        }
+        return r;
+      };
+      uint16_t &x = v[b.x], &y = v[b.y];
+      if (L.inv) {
+        y ^= x;
+        x ^= mulv(y);
+      } else {
+        x ^= mulv(y);
+        y ^= x;
+      }
+    }
+  };
+  auto rmul = [](uint16_t x, const uint32_t *M) -> uint16_t {  // the kernel's rmul on one symbol
+    const uint8_t u = x & 0xFF, v = x >> 8;
+    uint16_t r = 0;
+    for (int i = 0; i < 8; i++) {
+      int lo = 0, hi = 0;
+      for (int j = 0; j < 8; j++) {
+        lo ^= ((u >> j & 1) && (M[16 * i + j] & 0x0F0F0F0Fu)) ^ ((v >> j & 1) && (M[16 * i + 8 + j] & 0x0F0F0F0Fu));
+        hi ^= ((v >> j & 1) && (M[16 * i + j] & 0xF0F0F0F0u)) ^ ((u >> j & 1) && (M[16 * i + 8 + j] & 0xF0F0F0F0u));
+      }
+      r |= static_cast<uint16_t>(lo << i | hi << (8 + i));
+    }
+    return r;
+  };
+  std::vector<uint32_t> blk(decode_block_words(s));
+  for (int tr = 0; tr < trials; tr++) {
+    std::vector<uint16_t> data(k), par(m);
+    for (auto &x : data) x = static_cast<uint16_t>(rng());
+    scalar_encode(data.data(), k, m, false, false, par.data());
+    std::vector<uint8_t> present(k + m, 1);
+    std::vector<uint32_t> idx(k);
+    for (uint32_t i = 0; i < k; i++) idx[i] = i;
+    std::shuffle(idx.begin(), idx.end(), rng);
+    for (uint32_t i = 0; i < e; i++) present[idx[i]] = 0;
+    for (uint32_t p = 0; p < m - e; p++)  // drop some surplus recovery rows too
+      if (rng() % 4 == 0) present[k + rng() % m] = 0;
+    uint32_t have = 0;
+    for (uint32_t p = 0; p < m; p++) have += present[k + p];
+    if (have < e) continue;
+    if (decode_block(s, present.data(), blk.data()) != RS_OK) return ~0ull;
+    std::vector<uint16_t> d2 = data, enc(m);
+    for (uint32_t g = 0; g < k; g++)
+      if (!present[g]) d2[g] = 0;
+    scalar_encode(d2.data(), k, m, false, false, enc.data());
+    std::vector<uint16_t> a(C, 0);
+    for (uint32_t p = 0; p < m; p++)
+      if (blk[dwm + 1 + p / 32] >> (p % 32) & 1) a[p] = rmul(to_uv(par[p] ^ enc[p]), &blk[mko + 128 * p]);
+    for (const Layer &L : ifft_layers(C, m, 0)) apply(a, L);
+    for (uint32_t K = 1; K <= (k + C - 1) / C; K++) {
+      if (!(blk[dwm] >> K & 1)) continue;
+      const uint32_t tK = std::min<uint32_t>(C, k - (K - 1) * C);
+      std::vector<uint16_t> y = a;
+      for (const Layer &L : fft_layers(C, tK, static_cast<uint64_t>(K) * C)) apply(y, L);
+      for (uint32_t q = 0; q < tK; q++) {
+        const uint32_t g = (K - 1) * C + q;
+        if (present[g]) continue;
+        bad += to_uv(rmul(y[q], &blk[mko + 128 * (m + g)])) != data[g];
+      }
+    }
   }
   return bad;
 }

@@ -52,6 +52,12 @@ struct Spec {
   // per-stripe masks (launch dmask): the data positions skipped and the rows stored
   // come from each stripe's mask block instead of skip / out_mode (one stripe per unit)
   bool dyn = false;
+  // fused reconstruct (implies dyn, corrected multiply, no D2): the syndromes
+  // s = rec ^ Enc(d') of the rows R, then the reference's erasure-locator decode
+  // (root.zig:268-335) restricted to the residual codeword, which is zero on every
+  // received data position: x_g = (L'_g beta_K) * FFT_{C, skew KC}(IFFT_{C, skew 0}(L_R s_R))
+  // for erased g in data block K. The pattern is data (decode block).
+  bool decode = false;
 };
 // u32 words of a stripe's mask block (Spec::dyn): bit p of words [0, w - 2) = data shard
 // p read as zero, bit q of the last 2 words = parity row q stored
@@ -87,6 +93,31 @@ bool compile_check(const Spec &s, std::string &err, double *ms, size_t *code_byt
 hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uint64_t ds, const uint8_t *rec, uint64_t rs,
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st,
                   const uint32_t *dmask = nullptr, uint32_t dmask_words = 0, bool shared_mask = false);
+
+// ---- fused FFT reconstruct (Spec::decode). A pattern's decode block (u32 words):
+//   [0, dmw)            dyn mask words: bit p = data shard p erased (read as zero)
+//   [dmw]               bit K: data block K (positions [KC, KC + C)) has an erasure
+//   [dmw + 1, dmw + 3)  bit p: recovery row p is one of the rows R used
+//   [dmw + 3 + g]       output row of erased data shard g (0xFFFFFFFF: not erased)
+//   [mko + 128 p]       runtime-multiply masks (scalar_masks) of L_p, p < m (0 off R)
+//   [mko + 128 (m + g)] masks of L'_g * beta_K for erased g
+uint32_t decode_block_words(const Spec &s);
+uint32_t decode_mask_offset(const Spec &s);
+// beta_K for the W / C blocks of the decode transform (W = ceilPow2(C + k)); false if
+// the block structure does not reduce to one polynomial (it does for every code tried)
+bool decode_betas(uint32_t k, uint32_t m, std::vector<uint16_t> &beta);
+// the 128 nibble masks of multiplication by the element c in the kernel's (u|v) planes:
+// out_i = XOR_j (x_j & M[16 i + j]) ^ (swap(x_j) & M[16 i + 8 + j])
+void scalar_masks(uint16_t c, uint32_t *masks);
+// T's constants p_i = beta_{8+i} + beta_8 beta_i (u = lo ^ sum hi_i p_i): the device plan
+// kernel's (u|v) change of basis
+void uv_basis(uint32_t p[8]);
+// decode block of one erasure pattern (present: k + m flags) for e = #erased <= m;
+// R = the first e present recovery rows. Returns RS_OK or an RS_ERR_* status.
+int decode_block(const Spec &s, const uint8_t *present, uint32_t *blk);
+// scalar check of the decode schedule (host): mismatching symbols over `trials`
+// random stripes and patterns with e erasures
+uint64_t decode_selftest(uint32_t k, uint32_t m, uint32_t e, int trials);
 
 // Host check of the generator's arithmetic: runs the kernel's schedule with its
 // T-coordinate matrices on scalar symbols and compares with scalar_encode.

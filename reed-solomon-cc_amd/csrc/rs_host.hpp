@@ -135,6 +135,10 @@ struct DecodePlan {
   // polynomial form)
   std::shared_ptr<DevBuf> syn_blk;
   uint32_t syn_dmw = 0, syn_pw = 0, syn_cs = 0;
+  // the fused FFT reconstruct (fftnet::Spec::decode): the pattern's
+  // decode block (rows R, locator masks, output rows); the kernel is per code
+  std::shared_ptr<DevBuf> fdec_blk;
+  uint32_t fdec_words = 0;
 };
 
 // Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
@@ -232,11 +236,16 @@ void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 // (pattern-agnostic: compiled once per code; also the batch syndrome path's cold form)
 struct WpsSlot {
   std::shared_ptr<FftSlot> fft = std::make_shared<FftSlot>();
+  std::shared_ptr<FftSlot> dec = std::make_shared<FftSlot>();  // fused FFT reconstruct (corrected multiply)
   std::mutex mu;
   bool solve_failed = false;
 };
 void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<WpsSlot> &out);
 const jit::Kernel *wps_solve_kernel(WpsSlot &ws);
+// RS_AMD_FDEC: "0" never the fused FFT reconstruct, "1" whenever it applies, "auto"
+// (default) unless the pattern's e x e network is loaded
+int fdec_mode();
+bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags);
 // exp, log, log_walsh in HBM (384 KiB per device)
 int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw);
 

@@ -151,6 +151,20 @@ hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint
                            uint64_t n, const uint16_t *G, const uint16_t *d_exp, const uint16_t *d_log, uint32_t *plan,
                            uint32_t plan_dw, uint32_t dmw, int32_t *status, hipStream_t s);
 
+// Per-stripe decode blocks of the fused FFT reconstruct (fftnet::Spec::decode; layout of
+// fftnet::decode_block): trimmed [n][k+m] (scratch: the rows R = first e present
+// recovery rows), logs [n][W] (scratch), blk [n][words]. FdecConsts: beta_K per data
+// block (fftnet::decode_betas) and the (u|v) basis constants (rs_fftnet.cpp Basis::p).
+struct FdecConsts {
+  uint32_t beta[32];
+  uint32_t p[8];
+};
+hipError_t launch_fdec_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                            uint32_t W, uint64_t n, uint32_t max_e, const uint16_t *d_exp, const uint16_t *d_log,
+                            const uint16_t *d_log_walsh, uint8_t *trimmed, uint16_t *logs, uint32_t *blk,
+                            uint32_t dwm, uint32_t mko, uint32_t words, const FdecConsts &cst, int32_t *status,
+                            hipStream_t s);
+
 // present rows trimmed to the k shards the matrix path decodes from (out: [n][k+m])
 hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
                                uint8_t *out, hipStream_t s);

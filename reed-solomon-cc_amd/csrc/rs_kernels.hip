@@ -1832,6 +1832,96 @@ hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint
   return hipGetLastError();
 }
 
+// Per-stripe decode blocks of the fused FFT reconstruct (rs_fftnet.hpp decode_block, on
+// the device): one thread per (stripe, slot). Slot 0 writes the mask words, the block
+// mask, the rows R (the trimmed present rows), the output rows and the status; slot
+// 1 + p the masks of L_p (recovery row p in R); slot 1 + m + g those of
+// L'_g * beta_K (erased data shard g); unused slots write zero masks.
+__device__ uint32_t to_uv_d(uint32_t x, const FdecConsts &c) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) lo ^= (x >> (8 + i) & 1) ? c.p[i] : 0u;
+  return x ^ lo;
+}
+__global__ __launch_bounds__(256) void k_fdec_block(const uint8_t *__restrict__ trimmed, uint32_t k, uint32_t m,
+                                                    uint32_t C, uint32_t W, uint64_t n, uint32_t max_e,
+                                                    const uint16_t *__restrict__ logs, const uint16_t *__restrict__ exp,
+                                                    const uint16_t *__restrict__ log, uint32_t dwm, uint32_t mko,
+                                                    uint32_t words, uint32_t *__restrict__ blk, int32_t *status,
+                                                    FdecConsts cst) {
+  const uint64_t slots = 1ull + m + k, gi = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gi >= n * slots) return;
+  const uint64_t s = gi / slots;
+  const uint32_t slot = static_cast<uint32_t>(gi % slots);
+  const uint8_t *pr = trimmed + s * (k + m);
+  uint32_t *b = blk + s * words;
+  const uint16_t *lg = logs + s * W;
+  if (slot == 0) {
+    uint32_t e = 0, used = 0;
+    for (uint32_t g = 0; g < k; g++) e += pr[g] ? 0u : 1u;
+    for (uint32_t p = 0; p < m; p++) used += pr[k + p] ? 1u : 0u;
+    if (status) status[s] = used < e ? 2 : (e > max_e ? 14 : 0);  // NotEnoughShards / InvalidArgument
+    for (uint32_t i = 0; i < mko; i++) b[i] = 0;
+    for (uint32_t g = 0; g < k; g++) b[dwm + 3 + g] = 0xFFFFFFFFu;
+    if (used < e) return;  // nothing restored
+    uint32_t row = 0;  // more than max_e erased: the first max_e are restored (status 14)
+    for (uint32_t g = 0; g < k; g++)
+      if (!pr[g]) {
+        b[g / 32] |= 1u << (g % 32);
+        if (row < max_e) {
+          b[dwm + 3 + g] = row++;
+          b[dwm] |= 1u << ((C + g) / C);
+        }
+      }
+    for (uint32_t p = 0; p < m; p++)
+      if (pr[k + p]) b[dwm + 1 + p / 32] |= 1u << (p % 32);
+    return;
+  }
+  uint32_t c = 0;
+  if (slot <= m) {
+    const uint32_t p = slot - 1;
+    if (pr[k + p]) c = exp[lg[p]];  // root.zig:292-295
+  } else {
+    const uint32_t g = slot - 1 - m;
+    if (!pr[g]) c = mul16_d(cst.beta[(C + g) / C], 65535u - lg[C + g], exp, log);  // root.zig:321-326
+  }
+  uint32_t *M = b + mko + 128u * (slot - 1);
+  uint32_t cu[8], cv[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    cu[j] = c ? to_uv_d(mul16_d(to_uv_d(1u << j, cst), log[c], exp, log), cst) : 0u;
+    cv[j] = c ? to_uv_d(mul16_d(to_uv_d(1u << (8 + j), cst), log[c], exp, log), cst) : 0u;
+  }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 8; j++) {
+      M[16 * i + j] = ((cu[j] >> i & 1) ? 0x0F0F0F0Fu : 0u) | ((cv[j] >> (8 + i) & 1) ? 0xF0F0F0F0u : 0u);
+      M[16 * i + 8 + j] = ((cv[j] >> i & 1) ? 0x0F0F0F0Fu : 0u) | ((cu[j] >> (8 + i) & 1) ? 0xF0F0F0F0u : 0u);
+    }
+}
+
+hipError_t launch_fdec_plan(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
+                            uint32_t W, uint64_t n, uint32_t max_e, const uint16_t *d_exp, const uint16_t *d_log,
+                            const uint16_t *d_log_walsh, uint8_t *trimmed, uint16_t *logs, uint32_t *blk,
+                            uint32_t dwm, uint32_t mko, uint32_t words, const FdecConsts &cst, int32_t *status,
+                            hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (W / C > 32 || mko < dwm + 3 + k || words < mko + 128 * (m + k)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_trim_present, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, present,
+                     present_stride, k, m, n, trimmed);
+  hipError_t e = hipGetLastError();
+  for (uint64_t s0 = 0; e == hipSuccess && s0 < n; s0 += 65535) {
+    const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
+    hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, trimmed + s0 * (k + m), static_cast<uint64_t>(k + m),
+                       k, m, C, W, d_log_walsh, logs + s0 * W);
+    e = hipGetLastError();
+  }
+  if (e != hipSuccess) return e;
+  const uint64_t threads = n * (1ull + m + k);
+  hipLaunchKernelGGL(k_fdec_block, dim3(static_cast<uint32_t>((threads + 255) / 256)), dim3(256), 0, s, trimmed, k, m, C,
+                     W, n, max_e, logs, d_exp, d_log, dwm, mko, words, blk, status, cst);
+  return hipGetLastError();
+}
+
 hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
                                uint8_t *out, hipStream_t s) {
   hipLaunchKernelGGL(k_trim_present, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, present,

@@ -47,8 +47,32 @@ void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<W
     fs.m = static_cast<uint32_t>(m);
     fs.flags = flags & RS_FLAG_QUIRK_D2;
     fs.dyn = true;
+    fftnet::Spec &ds = p->dec->spec;
+    ds.k = static_cast<uint32_t>(k);
+    ds.m = static_cast<uint32_t>(m);
+    ds.dyn = ds.decode = true;
   }
   out = p;
+}
+
+int fdec_mode() {
+  const char *e = std::getenv("RS_AMD_FDEC");
+  if (e && std::strcmp(e, "0") == 0) return 0;
+  if (e && std::strcmp(e, "1") == 0) return 1;
+  return 2;
+}
+
+// corrected multiply only (under D1 the literal decode is no inverse of the encode), and
+// no code whose D2 encode drops a chunk (its parity is no codeword, so the result would
+// depend on which recovery rows are read; root.zig:268-335 reads all of them)
+bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
+  std::vector<uint16_t> beta;
+  const uint64_t C = ceil_pow2(m);
+  const bool d2_drops = (flags & RS_FLAG_QUIRK_D2) && k > C && k % C == 0;
+  return fdec_mode() != 0 && !(flags & RS_FLAG_QUIRK_D1) && !d2_drops && fft_enabled() &&
+         fftnet::supports(k, m, sb, true) &&
+         fftnet::pieces(sb) == 1 && sb % fftnet::kUnitBytes == 0 &&
+         fftnet::decode_betas(static_cast<uint32_t>(k), static_cast<uint32_t>(m), beta);
 }
 
 const jit::Kernel *wps_solve_kernel(WpsSlot &ws) {
@@ -138,6 +162,13 @@ bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t m
          m <= 64;  // max_e up to m: output groups of 8 (rs_psyn.hpp launch_solve)
 }
 
+// the fused FFT reconstruct with per-stripe decode blocks (any whole 2 KiB units)
+bool fdec_patterns_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
+  const char *pm = std::getenv("RS_AMD_PATTERNS");
+  const std::string mode = pm ? pm : "";
+  return (mode.empty() || mode == "auto" || mode == "psyn") && m <= 64 && fdec_supports(k, m, sb, flags);
+}
+
 bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
@@ -153,6 +184,8 @@ const char *rs_patterns_kernel_name(uint64_t k, uint64_t m, size_t sb, uint32_t 
   thread_local std::string name;
   if (psyn_enabled(k, m, sb, flags)) {
     name = "psyn_k" + std::to_string(k) + "_m" + std::to_string(m);
+  } else if (fdec_patterns_enabled(k, m, sb, flags)) {
+    name = "fft_decode";
   } else if (wps_enabled(k, m, sb, flags, max_e)) {
     name = "fft_syndromes+psyn_solve";
   } else {
@@ -243,6 +276,47 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
         if (e != hipSuccess) return hip_fail(e, "per-stripe syndrome network");
         return RS_OK;
       }
+    }
+    // wide codes: the fused FFT reconstruct with per-stripe decode blocks built on the GPU
+    // (trimmed rows R, erasure locator, masks)
+    if (max_nv == 4 && fdec_patterns_enabled(k, m, sb, flags)) {
+      std::shared_ptr<WpsSlot> ws;
+      wps_slot(dev, k, m, flags, ws);
+      const fftnet::Spec *dfs = nullptr;
+      if (const jit::Kernel *fk = fft_kernel(*ws->dec, sb, &dfs)) {
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const uint32_t words = fftnet::decode_block_words(*dfs), dwm = fftnet::dyn_mask_words(*dfs),
+                       mko = fftnet::decode_mask_offset(*dfs);
+        FdecConsts cst{};
+        std::vector<uint16_t> beta;
+        fftnet::decode_betas(static_cast<uint32_t>(k), static_cast<uint32_t>(m), beta);
+        for (size_t i = 0; i < beta.size() && i < 32; i++) cst.beta[i] = beta[i];
+        fftnet::uv_basis(cst.p);
+        // decode blocks in slices of <= 1 GiB
+        const uint64_t per_bytes = static_cast<uint64_t>(words) * 4 + (k + m) + W * 2;
+        const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, (1ull << 30) / per_bytes));
+        void *tmp = nullptr;
+        HIP_TRY(hipMallocAsync(&tmp, per * per_bytes + 256, s));
+        uint32_t *blk = static_cast<uint32_t *>(tmp);
+        uint16_t *logs = reinterpret_cast<uint16_t *>(blk + per * words);
+        uint8_t *trimmed = reinterpret_cast<uint8_t *>(logs + per * W);
+        hipError_t e = hipSuccess;
+        for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += per) {
+          const uint64_t cnt = std::min(per, n_stripes - s0);
+          e = launch_fdec_plan(d_present + s0 * present_stride, present_stride, static_cast<uint32_t>(k),
+                               static_cast<uint32_t>(m), static_cast<uint32_t>(C), static_cast<uint32_t>(W), cnt, max_e,
+                               dexp, dlog, dlw, trimmed, logs, blk, dwm, mko, words, cst,
+                               d_status ? d_status + s0 : nullptr, s);
+          if (e == hipSuccess)
+            e = fftnet::launch(*fk, *dfs, static_cast<const uint8_t *>(d_original) + s0 * orig_stride, orig_stride,
+                               static_cast<const uint8_t *>(d_recovery) + s0 * rec_stride, rec_stride,
+                               static_cast<uint8_t *>(d_restored) + s0 * out_stride, out_stride, sb, cnt, s, blk, words);
+        }
+        (void)hipFreeAsync(tmp, s);
+        if (e != hipSuccess) return hip_fail(e, "per-stripe fused FFT reconstruct");
+        return RS_OK;
+      }
+      if (fdec_mode() == 1) return fail(RS_ERR_DEVICE, "RS_AMD_FDEC=1: fused FFT reconstruct kernel unavailable");
     }
     // wide codes: syndromes on the FFT kernel (per-stripe masks), then the e x e solve
     if (max_nv == 4 && wps_enabled(k, m, sb, flags, max_e)) {

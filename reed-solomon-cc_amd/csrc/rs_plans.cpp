@@ -219,7 +219,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
                     std::to_string(jit::enabled() && jit::shard_ok(sb)) + "/" +
                     std::to_string(fft_enabled() && fftnet::supports(k, m, sb)) + "/" +
-                    std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/";
+                    std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/" +
+                    std::to_string(fdec_mode()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   {
@@ -264,6 +265,20 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     plan->inv_fft->spec.m = static_cast<uint32_t>(m);
     plan->inv_fft->spec.flags = flags;
     plan->inv_fft->spec.inverse = true;
+  }
+
+  // the fused FFT reconstruct's block for this pattern (wide codes): the
+  // form every pattern runs until a network compiled for it is loaded
+  if (e > 0 && m <= 64 && fdec_supports(k, m, sb, flags)) {
+    fftnet::Spec ds;
+    ds.k = static_cast<uint32_t>(k);
+    ds.m = static_cast<uint32_t>(m);
+    ds.dyn = ds.decode = true;
+    std::vector<uint32_t> blk(fftnet::decode_block_words(ds));
+    if (fftnet::decode_block(ds, present, blk.data()) == RS_OK) {
+      if (int st = upload(blk.data(), blk.size() * sizeof(uint32_t), dev, plan->fdec_blk)) return st;
+      plan->fdec_words = static_cast<uint32_t>(blk.size());
+    }
   }
 
   if (use_matrix) {
@@ -453,6 +468,35 @@ int rs_fft_selftest(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *skip,
     if (skip) spec.skip.assign(skip, skip + k);
     spec.inverse = check_inverse(k, m);
     const uint64_t bad = fftnet::selftest(spec, trials);
+    if (mismatches) *mismatches = bad;
+    return RS_OK;
+  });
+}
+
+int rs_fft_decode_compile_check(uint64_t k, uint64_t m, double *compile_ms, uint64_t *code_bytes) {
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, fftnet::kUnitBytes);
+    if (st) return st;
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes, true)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
+    fftnet::Spec spec;
+    spec.k = static_cast<uint32_t>(k);
+    spec.m = static_cast<uint32_t>(m);
+    spec.dyn = spec.decode = true;
+    std::string err;
+    size_t bytes = 0;
+    if (!fftnet::compile_check(spec, err, compile_ms, &bytes)) return fail(RS_ERR_DEVICE, err);
+    if (code_bytes) *code_bytes = bytes;
+    return RS_OK;
+  });
+}
+
+int rs_fft_decode_selftest(uint64_t k, uint64_t m, uint32_t e, int trials, uint64_t *mismatches) {
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, fftnet::kUnitBytes);
+    if (st) return st;
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes, true) || e > m || e > k || e == 0)
+      return fail(RS_ERR_INVALID_ARGUMENT, "no FFT decode form");
+    const uint64_t bad = fftnet::decode_selftest(static_cast<uint32_t>(k), static_cast<uint32_t>(m), e, trials);
     if (mismatches) *mismatches = bad;
     return RS_OK;
   });

@@ -93,6 +93,8 @@ def lib():
         "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
         "rs_patterns_kernel_name": (C.c_char_p, [u64, u64, sz, u32, u32]),
         "rs_fft_selftest": (C.c_int, [u64, u64, u32, vp, C.c_int, vp]),
+        "rs_fft_decode_compile_check": (C.c_int, [u64, u64, vp, vp]),
+        "rs_fft_decode_selftest": (C.c_int, [u64, u64, u32, C.c_int, vp]),
         "rs_lowrate_selftest": (C.c_int, [u64, u64, C.c_int, u64, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
         "rs_engine_ifft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
@@ -386,6 +388,20 @@ def fft_selftest(k, m, flags=0, skip=None, trials=8) -> int:
     bad = C.c_uint64()
     sk = None if skip is None else (C.c_uint8 * k)(*[1 if x else 0 for x in skip])
     _check(lib().rs_fft_selftest(k, m, flags, sk, trials, C.byref(bad)))
+    return bad.value
+
+
+def fft_decode_compile_check(k, m) -> dict:
+    """Generate + hipRTC-compile the fused FFT reconstruct kernel (no device)."""
+    ms, b = C.c_double(0), C.c_uint64(0)
+    _check(lib().rs_fft_decode_compile_check(k, m, C.byref(ms), C.byref(b)))
+    return {"compile_ms": ms.value, "code_bytes": b.value}
+
+
+def fft_decode_selftest(k, m, erased, trials=8) -> int:
+    """Host check of the fused FFT reconstruct's schedule: wrong restored symbols."""
+    bad = C.c_uint64(0)
+    _check(lib().rs_fft_decode_selftest(k, m, erased, trials, C.byref(bad)))
     return bad.value
 
 

@@ -111,7 +111,7 @@ def test_device_entry_points_fail_loudly_without_gpu():
         R.engine_mul_scalar(bytearray(64), 7)
 
 
-def test_kernel_selection_network():
+def test_kernel_selection_network(monkeypatch):
     """Bit-sliced network kernels (rs_jit.hpp) for shards in whole 4 KiB units and <= 16 outputs."""
     assert R.encode_kernel_name(10, 4, 1 << 20) == "net_encode_i10_o4"
     assert R.reconstruct_kernel_name(10, 4, 1 << 20) == "net_reconstruct_i10_o4"
@@ -128,13 +128,18 @@ def test_kernel_selection_network():
     # wide codes (chunk 32 / 64): the bit-sliced FFT kernel (rs_fftnet.hpp)
     assert R.encode_kernel_name(200, 55, 1 << 18) == "net_fft_encode_i200_o55"
     assert R.encode_kernel_name(100, 20, 1 << 18) == "net_fft_encode_i100_o20"
-    # wide code, 55 erasures: syndromes on the FFT kernel, the 55 x 55 map a (background-compiled) network
+    # wide code, 55 erasures: the fused FFT reconstruct (round 3) until the pattern's network
+    # is loaded; RS_AMD_FDEC=0: syndromes on the FFT kernel, the 55 x 55 map a
+    # (background-compiled) network
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "net_fft_decode_i200_o55"
+    monkeypatch.setenv("RS_AMD_FDEC", "0")
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+net_fft_encode_i200_o55+net_syndrome_i55_o55"
 
 
 def test_kernel_selection_async_cap(monkeypatch):
     """RS_AMD_NET_ASYNC_BLOCKS=0 keeps large maps on the table kernels."""
     monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
+    monkeypatch.setenv("RS_AMD_FDEC", "0")
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+net_fft_encode_i200_o55+decode_mtile16_nv1"
     monkeypatch.setenv("RS_AMD_FFT", "0")
     assert R.encode_kernel_name(100, 20, 1 << 18) == "encode_reg_w32_nv1"
@@ -221,22 +226,27 @@ def test_patterns_path_selection(monkeypatch):
     """rs_reconstruct_batch_dev_patterns' path per code (include/reedsol.h)."""
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "psyn_k10_m4"
     assert R.patterns_kernel_name(64, 4, 4096, 4) == "psyn_k64_m4"
-    assert R.patterns_kernel_name(200, 55, 1 << 18, 8) == "fft_syndromes+psyn_solve"
-    # max_e > 8: the solve runs in output groups of 8 (plan by one wave per stripe)
-    assert R.patterns_kernel_name(200, 55, 1 << 18, 9) == "fft_syndromes+psyn_solve"
-    assert R.patterns_kernel_name(200, 55, 1 << 18, 55) == "fft_syndromes+psyn_solve"
-    assert R.patterns_kernel_name(200, 55, 6144, 8) == "pattern_fft"  # no whole 4 KiB units
+    # wide codes (round 3): the fused FFT reconstruct with per-stripe decode blocks
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 8) == "fft_decode"
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 55) == "fft_decode"
+    assert R.patterns_kernel_name(200, 55, 6144, 8) == "fft_decode"  # whole 2 KiB units
+    assert R.patterns_kernel_name(200, 55, 5120, 8) == "pattern_fft"  # no whole 2 KiB units
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_matrix" or \
         R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_fft"  # D1: no syndrome network
     assert R.patterns_kernel_name(10, 4, 2048, 4) == "pattern_matrix"  # below the 4 KiB unit
     assert R.patterns_kernel_name(5, 5, 4096, 5) == "psyn_k5_m5"
-    # mid-band codes (round 3): the fused syndrome network for k <= 256, m <= 8; chunk-16
-    # FFT syndromes + the generic solve for 9 <= m <= 16
+    # mid-band codes (round 3): the fused syndrome network for k <= 256, m <= 8; the
+    # chunk-16 fused FFT reconstruct for 9 <= m <= 16
     assert R.patterns_kernel_name(100, 4, 1 << 20, 4) == "psyn_k100_m4"
     assert R.patterns_kernel_name(32, 8, 1 << 20, 8) == "psyn_k32_m8"
-    assert R.patterns_kernel_name(40, 12, 1 << 20, 12) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(40, 12, 1 << 20, 12) == "fft_decode"
+    assert R.patterns_kernel_name(16, 16, 1 << 20, 16) == "fft_decode"
+    assert R.patterns_kernel_name(64, 16, 1 << 20, 16) == "fft_decode"
+    # RS_AMD_FDEC=0: FFT syndromes + the generic e x e solve (max_e > 8: output groups of 8)
+    monkeypatch.setenv("RS_AMD_FDEC", "0")
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 9) == "fft_syndromes+psyn_solve"
     assert R.patterns_kernel_name(16, 16, 1 << 20, 16) == "fft_syndromes+psyn_solve"
-    assert R.patterns_kernel_name(64, 16, 1 << 20, 16) == "fft_syndromes+psyn_solve"
+    monkeypatch.delenv("RS_AMD_FDEC")
     assert R.patterns_kernel_name(300, 8, 1 << 20, 8) in ("pattern_matrix", "pattern_fft")  # k > 256
     monkeypatch.setenv("RS_AMD_PATTERNS", "fft")
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "pattern_fft"

@@ -20,6 +20,13 @@ from rs_amd import reedsol_amd as R  # noqa: E402
 DEV = torch.device("cuda:0")
 
 
+@pytest.fixture(autouse=True)
+def _syndrome_forms(monkeypatch):
+    """These tests cover the syndrome path's own forms (FFT syndromes + e x e map / solve /
+    table kernels); the fused FFT reconstruct has tests/test_gpu_fdec.py."""
+    monkeypatch.setenv("RS_AMD_FDEC", "0")
+
+
 def reconstruct(k, m, present, data, par, flags=0):
     n, _, sb = data.shape
     e = int(k - np.sum(present[:k]))
