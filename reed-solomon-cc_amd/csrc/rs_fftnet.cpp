@@ -999,7 +999,11 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       bool firstw = true;
       for (uint32_t w = 0; w < NW; w++) {
         if (P.posA(w, 0) >= tK) continue;
-        o << "  " << (firstw ? "if" : "else if") << " (w == " << w << "u) {\n";
+        // a wave whose 8 shards of the block are all received skips its layers (per-stripe
+        // patterns spread few losses over many blocks)
+        const uint32_t g0 = (K - 1) * C + 8 * w;
+        o << "  " << (firstw ? "if" : "else if") << " (w == " << w << "u) {\n  if ((DMc[" << g0 / 32 << "] >> "
+          << g0 % 32 << "u) & 0xFFu) {\n";
         firstw = false;
         bool z[8];
         for (uint32_t r = 0; r < 8; r++) {
@@ -1017,7 +1021,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         for (uint32_t r = 0; r < 8; r++)
           if (P.posA(w, r) < tK && z[r])
             for (int i = 0; i < 8; i++) o << "  " << wname(r) << "_" << i << " = 0u;\n";
-        o << "  }\n";
+        o << "  }\n  }\n";
       }
       // erased shards of the block: x_g = (L'_g beta_K) y_q, one code path for all waves
       g.ops = &g.st->ops_io;

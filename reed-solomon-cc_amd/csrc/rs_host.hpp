@@ -139,6 +139,9 @@ struct DecodePlan {
   // decode block (rows R, locator masks, output rows); the kernel is per code
   std::shared_ptr<DevBuf> fdec_blk;
   uint32_t fdec_words = 0;
+  // a pattern's first use builds only the fused block (no network spec, no tables: the
+  // host GF(2) algebra of those takes 10-40 ms); its next use builds the full plan
+  bool lite = false;
 };
 
 // Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
@@ -178,6 +181,12 @@ struct PlanCache {
     m.emplace(k, std::make_pair(v, ++tick));
     return v;
   }
+  std::shared_ptr<V> replace(const std::string &k, std::shared_ptr<V> v) {  // g_plan_mu held
+    auto it = m.find(k);
+    if (it == m.end()) return insert(k, v);
+    it->second = std::make_pair(v, ++tick);
+    return v;
+  }
   size_t size() const { return m.size(); }
 };
 
@@ -207,8 +216,9 @@ void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
 int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &ns);
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out);
+// full: never the lite plan (the fused kernel is unavailable)
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
-                    std::shared_ptr<DecodePlan> &out);
+                    std::shared_ptr<DecodePlan> &out, bool full = false);
 
 // ------------------------------------------------------ shard tails (rs_batch_dev.cpp)
 // Batches whose shard_bytes is not a multiple of 64 run on padded copies

@@ -162,11 +162,17 @@ bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t m
          m <= 64;  // max_e up to m: output groups of 8 (rs_psyn.hpp launch_solve)
 }
 
-// the fused FFT reconstruct with per-stripe decode blocks (any whole 2 KiB units)
-bool fdec_patterns_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
+// the fused FFT reconstruct with per-stripe decode blocks (any whole 2 KiB units). Its
+// decode tail costs about the same for any loss count (an IFFT plus one FFT per data block
+// with a loss), the generic solve grows with max_e^2: per-stripe RS(200,55) 256 KiB x 256
+// fused 9.9 vs 14.0 ms at max_e 55, 8.0 vs 4.8 ms at max_e 20; RS(64,64) max_e 40 4.7 vs
+// 4.0 ms (profiles/r03/fdec/). So auto takes it for max_e >= 3/4 m (and where the solve
+// has no 4 KiB units to run on); RS_AMD_FDEC=1 always.
+bool fdec_patterns_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t max_e) {
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
-  return (mode.empty() || mode == "auto" || mode == "psyn") && m <= 64 && fdec_supports(k, m, sb, flags);
+  if (!(mode.empty() || mode == "auto" || mode == "psyn") || m > 64 || !fdec_supports(k, m, sb, flags)) return false;
+  return fdec_mode() == 1 || 4ull * max_e >= 3ull * m || sb % jit::kUnitBytes != 0;
 }
 
 bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
@@ -184,7 +190,7 @@ const char *rs_patterns_kernel_name(uint64_t k, uint64_t m, size_t sb, uint32_t 
   thread_local std::string name;
   if (psyn_enabled(k, m, sb, flags)) {
     name = "psyn_k" + std::to_string(k) + "_m" + std::to_string(m);
-  } else if (fdec_patterns_enabled(k, m, sb, flags)) {
+  } else if (fdec_patterns_enabled(k, m, sb, flags, max_e)) {
     name = "fft_decode";
   } else if (wps_enabled(k, m, sb, flags, max_e)) {
     name = "fft_syndromes+psyn_solve";
@@ -279,7 +285,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     }
     // wide codes: the fused FFT reconstruct with per-stripe decode blocks built on the GPU
     // (trimmed rows R, erasure locator, masks)
-    if (max_nv == 4 && fdec_patterns_enabled(k, m, sb, flags)) {
+    if (max_nv == 4 && fdec_patterns_enabled(k, m, sb, flags, max_e)) {
       std::shared_ptr<WpsSlot> ws;
       wps_slot(dev, k, m, flags, ws);
       const fftnet::Spec *dfs = nullptr;

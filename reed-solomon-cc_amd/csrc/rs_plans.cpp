@@ -213,7 +213,7 @@ int syndrome_block(int dev, uint64_t k, uint64_t m, const uint8_t *present, cons
 // root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
 // kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
-                    std::shared_ptr<DecodePlan> &out) {
+                    std::shared_ptr<DecodePlan> &out, bool full) {
   const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
@@ -223,15 +223,41 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
                     std::to_string(fdec_mode()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
+  std::shared_ptr<DecodePlan> lite;
   {
     std::lock_guard<std::mutex> lk(g_plan_mu);
-    if ((out = g_dec_plans.find(key))) return RS_OK;
+    if ((out = g_dec_plans.find(key))) {
+      if (!out->lite) return RS_OK;
+      if (!full && fdec_mode() == 1) return RS_OK;  // forced fused form: the block is all it needs
+      lite = out;  // the pattern's second use: build the full plan (network, tables) now
+      out.reset();
+    }
   }
   const bool d1 = flags & RS_FLAG_QUIRK_D1;
   const uint64_t C = ceil_pow2(m), end = C + k, W = ceil_pow2(C + k);
   uint64_t e = 0, present_count = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
+  // first use of a wide-code pattern: only the fused FFT reconstruct's block
+  const bool every_lost = e == k && present_count == m;  // the inverse form's case stays on the full plan
+  if (!lite && !full && e > 0 && !every_lost && m <= 64 && fdec_supports(k, m, sb, flags) &&
+      (mode == "auto" || mode == "net")) {
+    auto plan = std::make_shared<DecodePlan>();
+    fftnet::Spec ds;
+    ds.k = static_cast<uint32_t>(k);
+    ds.m = static_cast<uint32_t>(m);
+    ds.dyn = ds.decode = true;
+    std::vector<uint32_t> blk(fftnet::decode_block_words(ds));
+    if (fftnet::decode_block(ds, present, blk.data()) == RS_OK) {
+      if (int st = upload(blk.data(), blk.size() * sizeof(uint32_t), dev, plan->fdec_blk)) return st;
+      plan->fdec_words = static_cast<uint32_t>(blk.size());
+      plan->lite = true;
+      plan->e = static_cast<uint32_t>(e);
+      std::lock_guard<std::mutex> lk(g_plan_mu);
+      out = g_dec_plans.insert(key, plan);
+      return RS_OK;
+    }
+  }
   int kind = decode_kind(k, m, flags, e, present_count, sb);
   // bit-sliced network (rs_jit.hpp): the same e x k map as the matrix kernels at a
   // fraction of their VALU cost, so preferred whenever it applies (modes auto / net)
@@ -269,7 +295,10 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
 
   // the fused FFT reconstruct's block for this pattern (wide codes): the
   // form every pattern runs until a network compiled for it is loaded
-  if (e > 0 && m <= 64 && fdec_supports(k, m, sb, flags)) {
+  if (lite) {
+    plan->fdec_blk = lite->fdec_blk;
+    plan->fdec_words = lite->fdec_words;
+  } else if (e > 0 && m <= 64 && fdec_supports(k, m, sb, flags)) {
     fftnet::Spec ds;
     ds.k = static_cast<uint32_t>(k);
     ds.m = static_cast<uint32_t>(m);
@@ -319,6 +348,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     if (use_net || use_net_async || syn_net) {
       plan->net = std::make_shared<NetSlot>();
       plan->net->async = !jit::supports(map.n_in, map.n_out, sb);
+      if (lite) plan->net->uses = 1;  // the lite plan's call was the pattern's first use
       plan->net->spec = std::move(map);
     }
     plan->e = static_cast<uint32_t>(n_out);
@@ -326,7 +356,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     plan->off_mat = 0;
     plan->off_src = tabs.size() * sizeof(RsTab);
     std::lock_guard<std::mutex> lk(g_plan_mu);
-    out = g_dec_plans.insert(key, plan);
+    out = lite ? g_dec_plans.replace(key, plan) : g_dec_plans.insert(key, plan);
     return RS_OK;
   }
 
@@ -373,7 +403,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   plan->off_src = off_src;
   plan->off_dst = off_dst;
   std::lock_guard<std::mutex> lk(g_plan_mu);
-  out = g_dec_plans.insert(key, plan);
+  out = lite ? g_dec_plans.replace(key, plan) : g_dec_plans.insert(key, plan);
   return RS_OK;
 }
 

@@ -735,6 +735,7 @@ def test_small_shard_syndrome_network(oracle, monkeypatch, sb, n):
     map on its small-shard network variant (inputs rec ^ scratch per 1 KiB piece),
     compiled synchronously; ragged stripe counts with a guard row; == table kernels."""
     monkeypatch.setenv("RS_AMD_JIT_SYNC", "1")
+    monkeypatch.setenv("RS_AMD_FDEC", "0")  # the syndrome path's forms (fused: test_gpu_fdec.py)
     k, m = 200, 55
     rng = np.random.default_rng(sb + n)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)

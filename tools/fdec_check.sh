@@ -18,6 +18,14 @@ for step in ${STEPS:-tests c4}; do
     tests) run fdec_tests 500 python -u -m pytest tests/test_gpu_fdec.py -x -v --timeout 200 --timeout-method thread ${PYK:+-k "$PYK"} || exit $? ;;
     c4) run fdec_c4 500 python -u tools/kernel_sweep.py --k 200 --m 55 --shard-bytes 262144 --stripes 256 \
           --erase 55:1:3 --nv 4 --rounds 3 --reps 3 --wait --var RS_AMD_FDEC=0,1 || exit $? ;;
+    prof) run fdec_prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$(pwd)/gpurun_out/fdec_prof" -o run -- \
+            python3 tools/kernel_sweep.py --k 200 --m 55 --shard-bytes 262144 --stripes 256 \
+            --erase 55:1:3 --nv 4 --rounds 2 --reps 3 --wait --var RS_AMD_FDEC=0,1 || exit $? ;;
+    sq) run fdec_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM \
+            --output-format csv -d "$(pwd)/gpurun_out/fdec_sq" -o run -- \
+            python3 tools/kernel_sweep.py --k 200 --m 55 --shard-bytes 262144 --stripes 256 \
+            --erase 55:1:3 --nv 4 --rounds 1 --reps 1 --var RS_AMD_FDEC=1 || exit $? ;;
+    cold) run fdec_cold 300 python3 -u tools/cold_patterns.py || exit $? ;;
   esac
 done
 exit 0
