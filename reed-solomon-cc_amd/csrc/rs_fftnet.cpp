@@ -305,6 +305,11 @@ int env_int(const char *name, int def) {
 }
 
 
+// butterflies between sched_barriers: 0 / 2 / 4 measured the same as 1 (RS(200,55) encode
+// 3.72 / 3.70 / 3.72 vs 3.69 ms, fused decode 6.86 / 6.89 / 6.89 vs 6.90 ms,
+// profiles/r03/negative/fft_sched_spacing.jsonl); 1 bounds the compile time
+int sched_of() { return 1; }
+
 int prefetch_of(const Spec &s) {
   // the decode tail keeps the IFFT result live across its blocks: no register room for
   // the next unit's loads (prefetch 2 spills, 0 does not: 241 VGPRs for RS(200,55))
@@ -453,13 +458,14 @@ struct Gen {
     op(8);
   }
 
-  int sched = 0;  // sched_barrier after every butterfly (bounds the scheduler's interleaving)
+  int sched = 0;  // sched_barrier every `sched` butterflies (bounds the scheduler's interleaving)
+  int nbf = 0;
 
   // one butterfly on named 8-dword positions with zero tracking
   void butterfly(const std::string &xn, bool &zx, const std::string &yn, bool &zy, bool inv, const Tw &t) {
     const auto X = regs(xn), Y = regs(yn);
     if (zx && zy) return;
-    if (sched) o << "  __builtin_amdgcn_sched_barrier(0);\n";
+    if (sched && ++nbf % sched == 0) o << "  __builtin_amdgcn_sched_barrier(0);\n";
     if (t.zero && st) st->xor_only++;
     if (inv) {  // ifftPartial, Generic.zig:171-192: y ^= x; x ^= M y
       if (!zx) {
@@ -538,7 +544,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   Plan P = make_plan(s);
   Gen g;
   g.st = stats;
-  g.sched = 1;  // sched_barrier per butterfly: bounds the scheduler's interleaving (compile time)
+  g.sched = sched_of();  // sched_barrier per butterfly: bounds the scheduler's interleaving (compile time)
   Stats dummy;
   if (!g.st) g.st = &dummy;
   std::ostringstream &o = g.o;
@@ -1072,7 +1078,7 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
-  std::string k = "fft3:p" + std::to_string(prefetch_of(s)) + ":" +
+  std::string k = "fft3:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +

@@ -268,6 +268,16 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   // past the synchronous cap: the same map compiled in the background, the matrix
   // kernel meanwhile (RS(200,55) losing 8: 400 blocks, against syndrome + encode)
   const bool use_net_async = !use_net && kind != 0 && direct_net_async(e, n_in_want, sb, mode, k, m, flags);
+  // a lite plan stays lite unless a network would beat the fused kernel: a direct map
+  // (few losses: RS(200,55) 256 KiB x 256 losing 8, 2.6 vs 4.5 ms) or the syndrome path's
+  // e x e map for e >= 3/4 m (55 losses 6.6 vs 6.9 ms; 20 losses the fused kernel wins, 4.9
+  // vs 6.2 ms; profiles/r03/fdec/). The others skip the host plan algebra (10-40 ms) and
+  // the background compile for good.
+  const bool syn_wins = syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
+  if (lite && !full && !use_net && !use_net_async && !syn_wins) {
+    out = lite;
+    return RS_OK;
+  }
   const bool use_syn = !use_net && !use_net_async && syndrome_pick(k, m, e, flags, sb, mode);
   if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
   // the syndromes' e x e map as a network too (its table kernel stays the fallback)

@@ -171,10 +171,17 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   if ((mode == "auto" || mode == "net") && jit::enabled() &&
       jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb))
     return net_name("reconstruct", k, e);
-  // wide codes: the fused FFT reconstruct, until a network for the pattern is loaded
-  if (m <= 64 && fdec_mode() != 0 && fdec_supports(k, m, sb, flags_none()) &&
-      (fdec_mode() == 1 || decode_kind(k, m, flags_none(), e, have, sb) != 0 || syndrome_pick(k, m, e, flags_none(), sb, mode)))
-    return net_name("fft_decode", k, m);
+  // wide codes: the fused FFT reconstruct (every pattern's first calls; the steady state
+  // unless a network beats it: a direct map for few losses, the syndrome e x e map for
+  // e >= 3/4 m — rs_plans.cpp get_decode_plan)
+  if (m <= 64 && fdec_mode() != 0 && fdec_supports(k, m, sb, flags_none()) && e > 0 && !(e == k && have == m) &&
+      (mode == "auto" || mode == "net")) {
+    const bool syn = syndrome_pick(k, m, e, flags_none(), sb, mode);
+    const bool direct = decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode, k, m, flags_none());
+    if (fdec_mode() == 1 || !(direct || (syn && 4 * e >= 3 * m && jit::enabled() &&
+                                         jit::supports_async(static_cast<uint32_t>(e), static_cast<uint32_t>(e), sb))))
+      return net_name("fft_decode", k, m);
+  }
   if (decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode, k, m, flags_none()))
     return net_name("reconstruct", k, e);
   if (syndrome_pick(k, m, e, flags_none(), sb, mode)) {
