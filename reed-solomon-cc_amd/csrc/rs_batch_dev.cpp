@@ -243,7 +243,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
         if (fdec_mode() == 1) return fail(RS_ERR_DEVICE, "RS_AMD_FDEC=1: fused FFT reconstruct kernel unavailable");
       }
     }
-    if (plan->lite && (st = get_decode_plan(dev, k, m, sb, flags, present, plan, true))) return st;
+    if (plan->lite && (st = get_decode_plan(dev, k, m, sb, flags, present, plan, 1))) return st;
     if (plan->net && !plan->syndrome && max_nv == 4) {
       if (const jit::Kernel *nk = net_kernel(*plan->net, sb)) {
         HIP_TRY(jit::launch(*nk, static_cast<const uint8_t *>(d_original), orig_stride,

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -140,8 +141,10 @@ struct DecodePlan {
   std::shared_ptr<DevBuf> fdec_blk;
   uint32_t fdec_words = 0;
   // a pattern's first use builds only the fused block (no network spec, no tables: the
-  // host GF(2) algebra of those takes 10-40 ms); its next use builds the full plan
+  // host GF(2) algebra of those takes 10-40 ms); where a network would beat the fused
+  // kernel, its next use has the full plan built on the background worker
   bool lite = false;
+  std::atomic<bool> upgrading{false};
 };
 
 // Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
@@ -216,9 +219,11 @@ void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
 int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &ns);
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out);
-// full: never the lite plan (the fused kernel is unavailable)
+// how: 0 the cached plan (a lite plan schedules its upgrade when a network would win),
+// 1 never a lite plan (the fused kernel is unavailable), 2 build the full plan now (the
+// background upgrade)
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
-                    std::shared_ptr<DecodePlan> &out, bool full = false);
+                    std::shared_ptr<DecodePlan> &out, int how = 0);
 
 // ------------------------------------------------------ shard tails (rs_batch_dev.cpp)
 // Batches whose shard_bytes is not a multiple of 64 run on padded copies

@@ -801,6 +801,7 @@ struct Job {
   std::function<std::string()> gen;  // the kernel source (generated on the worker)
   std::function<void(Kernel &)> fill;  // launch metadata of the built kernel
   int dev;
+  std::function<void()> host;  // a host job instead of a compile (run_host_job)
 };
 
 struct Worker {
@@ -845,6 +846,18 @@ struct Worker {
         j = std::move(queue.front());
         queue.pop_front();
       }
+      if (j.host) {  // host work on the worker (a plan build): no module to insert
+        if (hipSetDevice(j.dev) == hipSuccess) {
+          try {
+            j.host();
+          } catch (...) {  // the caller keeps what it had (the job was an improvement)
+          }
+        }
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_pending.erase(j.key);
+        g_cv.notify_all();
+        continue;
+      }
       std::string e;
       std::unique_ptr<Kernel> k;
       if (hipSetDevice(j.dev) == hipSuccess) {
@@ -874,6 +887,22 @@ bool env_on(const char *name) {
 }
 
 }  // namespace
+
+bool run_host_job(const std::string &key, std::function<void()> fn) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const std::string full = std::to_string(dev) + ":host:" + key;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_pending.count(full)) return true;
+  g_pending.insert(full);
+  try {
+    g_worker.push(Job{full, "", nullptr, nullptr, dev, std::move(fn)});
+  } catch (const std::exception &) {
+    g_pending.erase(full);
+    return false;
+  }
+  return true;
+}
 
 uint64_t max_async_blocks() {
   const int v = env_int("RS_AMD_NET_ASYNC_BLOCKS", -1);

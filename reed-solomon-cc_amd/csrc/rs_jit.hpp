@@ -103,8 +103,12 @@ bool compile_source_check(const std::string &src, std::string &err, double *ms, 
 // hipRTC compiles run, code objects found in the disk cache, modules loaded (this process)
 void compile_stats(uint64_t *compiles, uint64_t *disk_hits, uint64_t *modules);
 
-// Block until no background compile is running (rs_net_wait).
+// Block until no background compile or host job is running (rs_net_wait).
 void wait_pending();
+// Run `fn` on the background worker, in order with the compiles (the current device set),
+// once per key while pending; false if the worker is unavailable. At exit the queue is
+// dropped and a running job finishes before the HIP runtime's teardown (as a compile).
+bool run_host_job(const std::string &key, std::function<void()> fn);
 
 // Generate and compile `spec` with hipRTC only (no device needed): a build check.
 bool compile_check(const NetSpec &spec, std::string &err, double *ms, size_t *code_bytes);

@@ -213,7 +213,8 @@ int syndrome_block(int dev, uint64_t k, uint64_t m, const uint8_t *present, cons
 // root.zig:268-335 erasure pattern -> evalPoly -> masks and table block (FFT
 // kernels), or -> the reconstruct's linear map as an e x k matrix (matrix kernel).
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
-                    std::shared_ptr<DecodePlan> &out, bool full) {
+                    std::shared_ptr<DecodePlan> &out, int how) {
+  const bool full = how == 1;
   const std::string mode = decode_mode_env();
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(flags) + "/" + mode + "/" + std::to_string(sb % 512 == 0) + "/" +
@@ -276,6 +277,18 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   const bool syn_wins = syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
   if (lite && !full && !use_net && !use_net_async && !syn_wins) {
     out = lite;
+    return RS_OK;
+  }
+  if (lite && how == 0) {  // the full plan is built on the worker; the fused kernel meanwhile
+    out = lite;
+    if (!lite->upgrading.exchange(true)) {
+      std::vector<uint8_t> pres(present, present + k + m);
+      if (!jit::run_host_job("plan:" + key, [dev, k, m, sb, flags, pres] {
+            std::shared_ptr<DecodePlan> p;
+            (void)get_decode_plan(dev, k, m, sb, flags, pres.data(), p, 2);
+          }))
+        lite->upgrading = false;
+    }
     return RS_OK;
   }
   const bool use_syn = !use_net && !use_net_async && syndrome_pick(k, m, e, flags, sb, mode);
