@@ -28,5 +28,18 @@ for c in FETCH_SIZE WRITE_SIZE; do
   step pmc4_$c 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc4/$c" -o run -- \
       python3 "$R/tools/kernel_sweep.py" --k 200 --m 55 --shard-bytes 262144 --stripes 256 --erase 55:1:3 --nv 4 \
       --rounds 1 --reps 1 --wait || exit $?
+  # the fused FFT reconstruct of the same pattern (RS_AMD_FDEC=1: no syndrome scratch)
+  step pmc4f_$c 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc4f/$c" -o run -- \
+      python3 "$R/tools/kernel_sweep.py" --k 200 --m 55 --shard-bytes 262144 --stripes 256 --erase 55:1:3 --nv 4 \
+      --rounds 1 --reps 1 --var RS_AMD_FDEC=1 || exit $?
+done
+# SQ / LDS counters of the c4 FFT kernels (encode, fused reconstruct), one pass per group
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM"; do
+  i=$((i+1))
+  step sq4_$i 200 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/sq4/g$i" -o run -- \
+      python3 "$R/tools/kernel_sweep.py" --k 200 --m 55 --shard-bytes 262144 --stripes 256 --erase 55:1:3 --nv 4 \
+      --rounds 1 --reps 1 --var RS_AMD_FDEC=1 || exit $?
 done
 exit 0
