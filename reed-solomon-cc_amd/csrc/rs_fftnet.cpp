@@ -586,10 +586,18 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
        "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
        // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division in the loop)
-       "  const u64 ub = blockIdx.x, ue = n_units;\n"
+    << (s.blocked ?
+       // blocked walk: workgroup b takes units [b per, (b + 1) per), a stripe's units in a row
+       // (per-stripe decode blocks stay in the scalar cache)
+       "  const u64 per = (n_units + gridDim.x - 1) / gridDim.x, ub = (u64)blockIdx.x * per,\n"
+       "            ue = ub + per < n_units ? ub + per : n_units, step = 1;\n"
+       "  u64 stripe = ub / ups;\n"
+       "  u32 uu = (u32)(ub - stripe * ups);\n"
+       "  const u32 gdiv = 0, gmod = 1;\n" :
+       "  const u64 ub = blockIdx.x, ue = n_units, step = gridDim.x;\n"
        "  u64 stripe = blockIdx.x / ups;\n"
        "  u32 uu = blockIdx.x - (u32)stripe * ups;\n"
-       "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n"
+       "  const u32 gdiv = gridDim.x / ups, gmod = gridDim.x - gdiv * ups;\n")
     << 
        "  const __amdgpu_buffer_rsrc_t RZ = __builtin_amdgcn_make_buffer_rsrc((void *)data, (short)0, 0, 0x00020000);\n"
        "  v4 la0[8], lb0[8];\n"
@@ -601,7 +609,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // (loads emitted below, once emit_loads exists)
   std::ostringstream hdr2;
   hdr2 << "#pragma unroll 1\n"
-    << "  for (u64 u = ub; u < ue; u += gridDim.x) {\n"
+    << "  for (u64 u = ub; u < ue; u += step) {\n"
     << 
        "  u32 sbl = sb;\n"
        "  asm volatile(\"\" : \"+s\"(sbl));  // shard offsets are recomputed per unit (SALU), not hoisted into VGPRs\n"
@@ -795,8 +803,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   o << "  u64 stripe_n = stripe + gdiv;\n  u32 uu_n = uu + gmod;\n  if (uu_n >= ups) { uu_n -= ups; stripe_n++; }\n";
   if (pf) {
     o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = " << (two ? "loff" : "uon + 1024u") << ";\n";
-    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, "u + gridDim.x < ue");
-    if (dyn) o << "  const u32 *DMn = dm + ((u + gridDim.x < ue) ? stripe_n : 0ull) * dmw;\n";
+    rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, "u + step < ue");
+    if (dyn) o << "  const u32 *DMn = dm + ((u + step < ue) ? stripe_n : 0ull) * dmw;\n";
     emit_loads(0, 0, pf, "RDn", "uon", "uon1");
     o << "  }\n";
   }
@@ -1082,7 +1090,7 @@ std::string cache_key(const Spec &s) {
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
-                  (s.dyn ? "dyn:" : "") + (s.decode ? "dec:" : "");
+                  (s.dyn ? "dyn:" : "") + (s.decode ? "dec:" : "") + (s.blocked ? "blk:" : "");
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
   k.push_back(':');
   for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));

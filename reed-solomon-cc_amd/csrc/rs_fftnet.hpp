@@ -58,6 +58,9 @@ struct Spec {
   // received data position: x_g = (L'_g beta_K) * FFT_{C, skew KC}(IFFT_{C, skew 0}(L_R s_R))
   // for erased g in data block K. The pattern is data (decode block).
   bool decode = false;
+  // workgroup b walks units [b per, (b + 1) per) instead of b, b + grid, ...: one stripe's
+  // units in a row (per-stripe decode blocks stay in the scalar cache)
+  bool blocked = false;
 };
 // u32 words of a stripe's mask block (Spec::dyn): bit p of words [0, w - 2) = data shard
 // p read as zero, bit q of the last 2 words = parity row q stored

@@ -252,6 +252,7 @@ void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 struct WpsSlot {
   std::shared_ptr<FftSlot> fft = std::make_shared<FftSlot>();
   std::shared_ptr<FftSlot> dec = std::make_shared<FftSlot>();  // fused FFT reconstruct (corrected multiply)
+  std::shared_ptr<FftSlot> decb = std::make_shared<FftSlot>();  // the same, blocked unit walk (per-stripe blocks)
   std::mutex mu;
   bool solve_failed = false;
 };

@@ -51,6 +51,8 @@ void wps_slot(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<W
     ds.k = static_cast<uint32_t>(k);
     ds.m = static_cast<uint32_t>(m);
     ds.dyn = ds.decode = true;
+    p->decb->spec = ds;
+    p->decb->spec.blocked = true;
   }
   out = p;
 }
@@ -164,15 +166,16 @@ bool wps_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t m
 
 // the fused FFT reconstruct with per-stripe decode blocks (any whole 2 KiB units). Its
 // decode tail costs about the same for any loss count (an IFFT plus one FFT per data block
-// with a loss), the generic solve grows with max_e^2: per-stripe RS(200,55) 256 KiB x 256
-// fused 9.9 vs 14.0 ms at max_e 55, 8.0 vs 4.8 ms at max_e 20; RS(64,64) max_e 40 4.7 vs
-// 4.0 ms (profiles/r03/fdec/). So auto takes it for max_e >= 3/4 m (and where the solve
-// has no 4 KiB units to run on); RS_AMD_FDEC=1 always.
+// with a loss), the generic solve grows with max_e^2. Per-stripe random patterns, 256 KiB
+// x 256 (profiles/r03/fdec/patterns_*.jsonl), fused vs solve: RS(200,55) max_e 20 / 30 /
+// 40 / 55: 6.6 / 6.9 / 7.3 / 7.7 vs 4.8 / 6.6 / 9.0 / 14.0 ms; RS(64,64) max_e 20 / 40:
+// 3.0 / 3.6 vs 2.2 / 4.0 ms; RS(100,20) max_e 20: 3.2 vs 3.3 ms. So auto takes it for
+// max_e >= 0.6 m (and where the solve has no 4 KiB units to run on); RS_AMD_FDEC=1 always.
 bool fdec_patterns_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, uint32_t max_e) {
   const char *pm = std::getenv("RS_AMD_PATTERNS");
   const std::string mode = pm ? pm : "";
   if (!(mode.empty() || mode == "auto" || mode == "psyn") || m > 64 || !fdec_supports(k, m, sb, flags)) return false;
-  return fdec_mode() == 1 || 4ull * max_e >= 3ull * m || sb % jit::kUnitBytes != 0;
+  return fdec_mode() == 1 || 5ull * max_e >= 3ull * m || sb % jit::kUnitBytes != 0;
 }
 
 bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
@@ -289,7 +292,11 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       std::shared_ptr<WpsSlot> ws;
       wps_slot(dev, k, m, flags, ws);
       const fftnet::Spec *dfs = nullptr;
-      if (const jit::Kernel *fk = fft_kernel(*ws->dec, sb, &dfs)) {
+      // blocked unit walk: a workgroup takes one stripe's units in a row, so the stripe's
+      // decode block stays in the scalar cache (RS(200,55) max_e 55: 10.0 -> 7.7 ms,
+      // RS(64,64) max_e 40: 4.75 -> 3.59 ms; for a batch-wide block it changes nothing,
+      // 6.91 vs 6.91 ms; profiles/r03/fdec/)
+      if (const jit::Kernel *fk = fft_kernel(*ws->decb, sb, &dfs)) {
         hipStream_t s = static_cast<hipStream_t>(stream);
         const uint32_t words = fftnet::decode_block_words(*dfs), dwm = fftnet::dyn_mask_words(*dfs),
                        mko = fftnet::decode_mask_offset(*dfs);

@@ -229,11 +229,11 @@ def test_patterns_path_selection(monkeypatch):
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4) == "psyn_k10_m4"
     assert R.patterns_kernel_name(64, 4, 4096, 4) == "psyn_k64_m4"
     # wide codes (round 3): the fused FFT reconstruct with per-stripe decode blocks for
-    # max_e >= 3/4 m, FFT syndromes + the generic solve below that
+    # max_e >= 0.6 m, FFT syndromes + the generic solve below that
     assert R.patterns_kernel_name(200, 55, 1 << 18, 8) == "fft_syndromes+psyn_solve"
     assert R.patterns_kernel_name(200, 55, 1 << 18, 55) == "fft_decode"
-    assert R.patterns_kernel_name(200, 55, 1 << 18, 42) == "fft_decode"
-    assert R.patterns_kernel_name(200, 55, 1 << 18, 40) == "fft_syndromes+psyn_solve"
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 33) == "fft_decode"
+    assert R.patterns_kernel_name(200, 55, 1 << 18, 32) == "fft_syndromes+psyn_solve"
     assert R.patterns_kernel_name(200, 55, 6144, 8) == "fft_decode"  # whole 2 KiB units
     assert R.patterns_kernel_name(200, 55, 5120, 8) == "pattern_fft"  # no whole 2 KiB units
     assert R.patterns_kernel_name(10, 4, 1 << 20, 4, 1) == "pattern_matrix" or \
