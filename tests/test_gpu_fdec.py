@@ -131,3 +131,48 @@ def test_fdec_per_stripe_patterns(oracle, monkeypatch, k, m, sb, n, max_e):
         got = missing[:max_e]
         assert (out[s, :len(got)] == data[s, got]).all(), (s, missing)
         assert (out[s, len(got):] == 0xAB).all(), s
+
+
+def _random_code(rng):
+    c = int(rng.choice([16, 32, 64]))
+    m = int(rng.integers(c // 2 + 1, c + 1))
+    while True:
+        k = int(rng.integers(1, min(16 * c, 300) + 1))
+        pk = 1 << (k - 1).bit_length()
+        if pk > c or (pk == c and k <= m):
+            return k, m
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fdec_fuzz(oracle, monkeypatch, seed):
+    """Seeded fuzz of the forced fused FFT reconstruct: random high-rate codes of chunk
+    16 / 32 / 64, shards of 1-6 whole 2 KiB units, 1-4 stripes, one batch pattern and one
+    pattern per stripe (random data and recovery losses), against the data (MDS)."""
+    monkeypatch.setenv("RS_AMD_FDEC", "1")
+    rng = np.random.default_rng(0xFDEC + seed)
+    k, m = _random_code(rng)
+    sb, n = 2048 * int(rng.integers(1, 7)), int(rng.integers(1, 5))
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=4)
+    e = int(rng.integers(1, min(k, m) + 1))
+    present = np.ones(k + m, np.uint8)
+    present[rng.choice(k, size=e, replace=False)] = 0
+    present[k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
+    got = reconstruct(k, m, present, data, par)
+    assert (got == data[:, present[:k] == 0]).all(), (k, m, sb, n, e)
+    pres = np.ones((n, k + m), np.uint8)
+    for s in range(n):
+        es = int(rng.integers(0, min(k, m) + 1))
+        pres[s, rng.choice(k, size=es, replace=False)] = 0
+        pres[s, k + rng.choice(m, size=int(rng.integers(0, m - es + 1)), replace=False)] = 0
+    max_e = int((pres[:, :k] == 0).sum(1).max()) or 1
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)  # noqa: E731
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, dev(pres), dev(data), dev(par), out, status)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    for s in range(n):
+        missing = [i for i in range(k) if not pres[s, i]]
+        assert status[s] == 0, (s, k, m)
+        assert (out[s, :len(missing)] == data[s, missing]).all(), (seed, s, k, m, sb, missing)
