@@ -226,7 +226,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     // the fused FFT reconstruct (wide codes): syndromes and decode in one kernel, the
     // pattern as data. RS_AMD_FDEC=auto runs it until a network compiled
     // for the pattern is loaded (as fast for the syndrome maps, faster for few losses)
-    if (plan->fdec_blk && max_nv == 4) {
+    if (plan->fdec_blk && max_nv == 4 && fdec_supports(k, m, sb, flags)) {
       const jit::Kernel *nk = plan->net && fdec_mode() != 1 ? net_kernel(*plan->net, sb) : nullptr;
       if (!nk) {
         std::shared_ptr<WpsSlot> ws;

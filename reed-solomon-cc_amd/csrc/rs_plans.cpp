@@ -221,7 +221,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
                     std::to_string(jit::enabled() && jit::shard_ok(sb)) + "/" +
                     std::to_string(fft_enabled() && fftnet::supports(k, m, sb)) + "/" +
                     std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/" +
-                    std::to_string(fdec_mode()) + "/";
+                    std::to_string(fdec_mode()) + "/" + std::to_string(fdec_supports(k, m, sb, flags)) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::shared_ptr<DecodePlan> lite;

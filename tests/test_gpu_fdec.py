@@ -176,3 +176,19 @@ def test_fdec_fuzz(oracle, monkeypatch, seed):
         missing = [i for i in range(k) if not pres[s, i]]
         assert status[s] == 0, (s, k, m)
         assert (out[s, :len(missing)] == data[s, missing]).all(), (seed, s, k, m, sb, missing)
+
+
+def test_fdec_pattern_across_shard_sizes(oracle):
+    """One pattern used with 2 KiB-unit shards (fused kernel) and then with 1 KiB shards
+    (no fused form: two stripes per unit) in the same process: each call takes a form that
+    fits its shard size (the plan cache keys on it)."""
+    k, m = 100, 20
+    lost = list(range(0, 100, 6))[:15]
+    present = np.ones(k + m, np.uint8)
+    present[lost] = 0
+    rng = np.random.default_rng(1024)
+    for sb in (2048, 1024, 6144):
+        data = rng.integers(0, 256, (3, k, sb), dtype=np.uint8)
+        par = oracle.encode_batch(k, m, data, threads=4)
+        for _ in range(2):
+            assert (reconstruct(k, m, present, data, par) == data[:, lost]).all(), sb
