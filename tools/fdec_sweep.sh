@@ -1,3 +1,7 @@
+#!/bin/bash
+# Round-3 A/B that chose the blocked unit walk for per-stripe fused decode blocks
+# (profiles/r03/fdec/blocked_and_shared_sweep.log). RS_AMD_FDEC_BLOCKED was a temporary
+# switch, removed once measured: re-running this needs it back in rs_patterns.cpp.
 mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fdec.py -q --timeout 200 --timeout-method thread > gpurun_out/t11.log 2>&1; tail -2 gpurun_out/t11.log || exit 1
 export RS_AMD_FDEC=1

@@ -17,7 +17,7 @@ for step in ${STEPS:-bench synform low}; do
   case $step in
     bench) run bench 500 python -u bench.py || exit $? ;;
     synform) run synform 400 python -u tools/kernel_sweep.py --k 200 --m 55 --shard-bytes 262144 --stripes 256 \
-               --erase 55:1:3 --nv 4 --rounds 3 --reps 3 --wait --var RS_AMD_SYN_FORM=auto,dyn,solve,cold || exit $? ;;
+               --erase 55:1:3 --nv 4 --rounds 3 --reps 3 --wait --var RS_AMD_FDEC=0,1 || exit $? ;;  # (round 3 first compared RS_AMD_SYN_FORM forms, since removed)
     low) for shape in "300 1000 65536 8 100:0:3" "200 1000 65536 8 100:0:2" "1000 4000 4096 64 300:0:3" \
                       "32 1000 65536 16 20:0:1" "16 4000 16384 16 8:0:2" "10 60 1048576 64 8:0:1"; do
            set -- $shape
