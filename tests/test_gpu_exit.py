@@ -2,7 +2,10 @@
 (rs_jit.cpp Worker: its exit handler drops the queue and joins the compile in flight
 before the HIP runtime is torn down). Before that handler, such an exit crashed in
 teardown (SIGSEGV after the results were printed): the host-memory path of
-tools/e2e_bench.py on RS(200,55), reproduced here."""
+tools/e2e_bench.py on RS(200,55), reproduced here. Since round 3 the pattern's first call
+runs the fused FFT reconstruct and its second queues the full plan's build as a host job
+on the same worker (then the 200 -> 4 network's compile), so the exit also lands while
+that job or the compile is in flight."""
 import os
 import subprocess
 import sys
