@@ -579,11 +579,10 @@ int rso_encode_low(uint64_t k, uint64_t m, size_t shard_bytes, const uint8_t *co
 /* Decoder.decode on a prepared work buffer (root.zig:268-335).
  * work: [Wdec][L][64]; received[pos] marks present positions (recovery at
  * [0,m), originals at [chunk, chunk+k)). Restored originals land in place. */
-static void decode_work(uint8_t *work, size_t L, uint64_t k, uint64_t m, const uint8_t *received,
-                        uint16_t *erasures, int quirks) {
+/* root.zig:277-289: the erasure flags of a received pattern -> evalPoly (logs) */
+static void decode_erasures(uint64_t k, uint64_t m, const uint8_t *received, uint16_t *erasures) {
   uint64_t chunk = ceil_pow2(m);
   uint64_t original_end = chunk + k;
-  uint64_t work_count = ceil_pow2(chunk + k);
   memset(erasures, 0, GF_ORDER * sizeof(uint16_t));
   for (uint64_t i = 0; i < m; i++) /* root.zig:278-287 */
     if (!received[i]) erasures[i] = 1;
@@ -591,6 +590,15 @@ static void decode_work(uint8_t *work, size_t L, uint64_t k, uint64_t m, const u
   for (uint64_t i = chunk; i < original_end; i++)
     if (!received[i]) erasures[i] = 1;
   rso_eval_poly(erasures, original_end); /* root.zig:289 */
+}
+
+/* the rest of Decoder.decode for erasures already evaluated (decode_erasures): a batch with
+ * one erasure pattern evaluates the locator once, as a batched caller of the reference would */
+static void decode_work_er(uint8_t *work, size_t L, uint64_t k, uint64_t m, const uint8_t *received,
+                           const uint16_t *erasures, int quirks) {
+  uint64_t chunk = ceil_pow2(m);
+  uint64_t original_end = chunk + k;
+  uint64_t work_count = ceil_pow2(chunk + k);
   for (uint64_t i = 0; i < m; i++) {     /* root.zig:292-303 */
     if (received[i]) rso_mul_scalar(SHARD(work, L, i), L, erasures[i], quirks);
     else memset(SHARD(work, L, i), 0, L * 64);
@@ -609,6 +617,12 @@ static void decode_work(uint8_t *work, size_t L, uint64_t k, uint64_t m, const u
   rso_fft(work, L, 0, work_count, original_end, 0, quirks); /* root.zig:318 */
   for (uint64_t i = chunk; i < original_end; i++)          /* root.zig:321-326 */
     if (!received[i]) rso_mul_scalar(SHARD(work, L, i), L, (uint16_t)(GF_MODULUS - erasures[i]), quirks);
+}
+
+static void decode_work(uint8_t *work, size_t L, uint64_t k, uint64_t m, const uint8_t *received,
+                        uint16_t *erasures, int quirks) {
+  decode_erasures(k, m, received, erasures);
+  decode_work_er(work, L, k, m, received, erasures, quirks);
 }
 
 /* top-level decode (root.zig:32-84) generalised to any even shard_bytes */
@@ -695,20 +709,16 @@ static void *batch_worker(void *arg) {
     uint16_t *erasures = malloc(GF_ORDER * sizeof(uint16_t));
     uint64_t e = 0;
     for (uint64_t i = 0; i < k; i++) e += !j->present[i];
+    for (uint64_t i = 0; i < k; i++) received[chunk + i] = j->present[i] != 0;
+    for (uint64_t i = 0; i < m; i++) received[i] = j->present[k + i] != 0;
+    decode_erasures(k, m, received, erasures); /* one pattern for the whole batch */
     for (size_t s = j->s_begin; s < j->s_end; s++) {
       const uint8_t *src = j->in + s * (k + m) * sb;
-      memset(received, 0, wc);
       for (uint64_t i = 0; i < k; i++)
-        if (j->present[i]) {
-          insert_shard(SHARD(work, L, chunk + i), src + i * sb, sb);
-          received[chunk + i] = 1;
-        }
+        if (j->present[i]) insert_shard(SHARD(work, L, chunk + i), src + i * sb, sb);
       for (uint64_t i = 0; i < m; i++)
-        if (j->present[k + i]) {
-          insert_shard(SHARD(work, L, i), src + (k + i) * sb, sb);
-          received[i] = 1;
-        }
-      decode_work(work, L, k, m, received, erasures, j->quirks);
+        if (j->present[k + i]) insert_shard(SHARD(work, L, i), src + (k + i) * sb, sb);
+      decode_work_er(work, L, k, m, received, erasures, j->quirks);
       uint64_t o = 0;
       for (uint64_t i = 0; i < k; i++)
         if (!j->present[i]) extract_shard(j->out + (s * e + o++) * sb, SHARD(work, L, chunk + i), sb);
