@@ -620,90 +620,194 @@ __device__ __forceinline__ void st(uint8_t *p, const Sym<NV> &s) {
   *reinterpret_cast<V *>(p + 32) = hi;
 }
 
-// Generic.zig:80-147 on positions base + p*ps (runtime size / truncation)
-template <int NV>
-__device__ void ifft_mem(uint8_t *w, uint64_t ps, uint64_t pos, uint64_t size, uint64_t trunc,
-                         const RsTab *__restrict__ tabs) {
-  uint64_t ti = 0, d = 1;
-  for (uint64_t d4 = 4; d4 <= size; d = d4, d4 <<= 2) {
-    const uint64_t rmax = trunc < size ? trunc : size;
-    for (uint64_t r = 0; r < rmax; r += d4) {
-      const RsTab *g = tabs + ti + 3 * (r / d4);
-      const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
-      for (uint64_t i = r; i < r + d; i++) {
-        uint8_t *p0 = w + (pos + i) * ps, *p1 = p0 + d * ps, *p2 = p1 + d * ps, *p3 = p2 + d * ps;
-        Sym<NV> s0, s1, s2, s3;
-        ld(s0, p0);
-        ld(s1, p1);
-        ld(s2, p2);
-        ld(s3, p3);
-        dev::ifft_bf(s0, s1, m01);
-        dev::ifft_bf(s2, s3, m23);
-        dev::ifft_bf(s0, s2, m02);
-        dev::ifft_bf(s1, s3, m02);
-        st(p0, s0);
-        st(p1, s1);
-        st(p2, s2);
-        st(p3, s3);
+// ---- the column transforms, phased (Generic.zig:15-147, runtime size / truncation).
+// A layer-by-layer walk reads and writes the whole column once per layer (5 passes
+// for 512 points). Here consecutive layers are grouped into phases whose butterflies
+// close over n <= 64 positions pos0 + j*dlo (j < n): a phase loads such a set into
+// VGPRs, runs its layers there (the j-space structure is exactly ifft_regs<n> /
+// fft_regs<n>; twiddle groups and truncation use the real positions) and stores it
+// back: 2 passes for 512 or 4,096 points. The first phase may read another buffer
+// (positions >= n_src read as zero) and the last may write another (positions
+// >= n_out dropped; out_sym: the shard layout of dev::store_sym), so a transform
+// between buffers costs no copy pass.
+__device__ __forceinline__ uint32_t log2_u64(uint64_t x) { return 63u - static_cast<uint32_t>(__builtin_clzll(x)); }
+
+// Generic.zig:80-147 on one position set (ti: table index of the phase's first layer)
+template <int N, int NV>
+__device__ __forceinline__ void ifft_sub(Sym<NV> *s, const RsTab *__restrict__ tabs, uint64_t ti, uint64_t size,
+                                         uint64_t rmax, uint64_t blk, uint32_t dlo_log) {
+  int jd = 1;
+#pragma unroll
+  for (int jd4 = 4; jd4 <= N; jd4 <<= 2) {
+    const uint32_t lg4 = static_cast<uint32_t>(__builtin_ctz(jd4)) + dlo_log;
+#pragma unroll
+    for (int jr = 0; jr < N; jr += jd4) {
+      const uint64_t r = blk + (static_cast<uint64_t>(jr) << dlo_log);
+      if (r < rmax) {
+        const RsTab *g = tabs + ti + 3 * (r >> lg4);
+        const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+#pragma unroll
+        for (int i = jr; i < jr + jd; i++) {
+          dev::ifft_bf(s[i], s[i + jd], m01);
+          dev::ifft_bf(s[i + 2 * jd], s[i + 3 * jd], m23);
+          dev::ifft_bf(s[i], s[i + 2 * jd], m02);
+          dev::ifft_bf(s[i + jd], s[i + 3 * jd], m02);
+        }
       }
     }
-    ti += 3 * (size / d4);
+    ti += 3 * (size >> lg4);
+    jd = jd4;
   }
-  if (d < size) {
+  if (jd < N) {  // the final odd layer (distance size/2): one table, no truncation
     const Tab t = dev::load_tab(tabs + ti);
-    for (uint64_t i = 0; i < d; i++) {
-      uint8_t *p0 = w + (pos + i) * ps, *p1 = w + (pos + d + i) * ps;
-      Sym<NV> s0, s1;
-      ld(s0, p0);
-      ld(s1, p1);
-      dev::ifft_bf(s0, s1, t);
-      st(p0, s0);
-      st(p1, s1);
+#pragma unroll
+    for (int i = 0; i < jd; i++) dev::ifft_bf(s[i], s[jd + i], t);
+  }
+}
+
+// Generic.zig:15-78 on one position set
+template <int N, int NV>
+__device__ __forceinline__ void fft_sub(Sym<NV> *s, const RsTab *__restrict__ tabs, uint64_t ti, uint64_t size,
+                                        uint64_t rmax, uint64_t blk, uint32_t dlo_log) {
+  int jd4 = N;
+#pragma unroll
+  for (int jd = N >> 2; jd != 0; jd >>= 2) {
+    const uint32_t lg4 = static_cast<uint32_t>(__builtin_ctz(jd4)) + dlo_log;
+#pragma unroll
+    for (int jr = 0; jr < N; jr += jd4) {
+      const uint64_t r = blk + (static_cast<uint64_t>(jr) << dlo_log);
+      if (r < rmax) {
+        const RsTab *g = tabs + ti + 3 * (r >> lg4);
+        const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
+#pragma unroll
+        for (int i = jr; i < jr + jd; i++) {
+          dev::fft_bf(s[i], s[i + 2 * jd], m02);
+          dev::fft_bf(s[i + jd], s[i + 3 * jd], m02);
+          dev::fft_bf(s[i], s[i + jd], m01);
+          dev::fft_bf(s[i + 2 * jd], s[i + 3 * jd], m23);
+        }
+      }
+    }
+    ti += 3 * (size >> lg4);
+    jd4 = jd;
+  }
+  if (jd4 == 2) {  // radix-2 tail (distance 1, so dlo == 1): a table per pair
+#pragma unroll
+    for (int jr = 0; jr < N; jr += 2) {
+      const uint64_t r = blk + static_cast<uint64_t>(jr);
+      if (r < rmax) {
+        const Tab t = dev::load_tab(tabs + ti + r / 2);
+        dev::fft_bf(s[jr], s[jr + 1], t);
+      }
     }
   }
 }
 
-// Generic.zig:15-78
+struct XformIO {
+  // buffers are wave-uniform bases; a lane adds `off` (global_load saddr + voffset form)
+  const uint8_t *src;  // first phase input (positions >= n_src read as zero)
+  uint64_t src_ps, n_src;
+  uint8_t *work;       // intermediate phases (in place)
+  uint64_t work_ps;
+  uint8_t *out;        // last phase output (positions >= n_out not stored)
+  uint64_t out_ps, n_out;
+  bool out_sym, contig;  // out in the shard layout (dev::store_sym) instead of work's
+  uint32_t off;          // the lane's byte offset in every buffer
+};
+
+// a lane's dword pair(s) at row + off (split layout) through a buffer resource whose base
+// is the wave-uniform row address: the loads keep the SGPR base + 32-bit lane offset form
+// (a plain pointer walk gets its per-lane 64-bit address math hoisted into VGPRs)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t *row) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(row), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
+}
 template <int NV>
-__device__ void fft_mem(uint8_t *w, uint64_t ps, uint64_t pos, uint64_t size, uint64_t trunc,
-                        const RsTab *__restrict__ tabs) {
-  uint64_t ti = 0, d4 = size;
-  for (uint64_t d = size >> 2; d != 0; d4 = d, d >>= 2) {
-    const uint64_t rmax = trunc < size ? trunc : size;
-    for (uint64_t r = 0; r < rmax; r += d4) {
-      const RsTab *g = tabs + ti + 3 * (r / d4);
-      const Tab m01 = dev::load_tab(g), m02 = dev::load_tab(g + 1), m23 = dev::load_tab(g + 2);
-      for (uint64_t i = r; i < r + d; i++) {
-        uint8_t *p0 = w + (pos + i) * ps, *p1 = p0 + d * ps, *p2 = p1 + d * ps, *p3 = p2 + d * ps;
-        Sym<NV> s0, s1, s2, s3;
-        ld(s0, p0);
-        ld(s1, p1);
-        ld(s2, p2);
-        ld(s3, p3);
-        dev::fft_bf(s0, s2, m02);
-        dev::fft_bf(s1, s3, m02);
-        dev::fft_bf(s0, s1, m01);
-        dev::fft_bf(s2, s3, m23);
-        st(p0, s0);
-        st(p1, s1);
-        st(p2, s2);
-        st(p3, s3);
+__device__ __forceinline__ void ldb(Sym<NV> &s, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  static_assert(NV == 1, "generic column walk: one dword pair per lane");
+  s.l[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  s.h[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 32u, 0, 0);
+}
+template <int NV>
+__device__ __forceinline__ void stb(__amdgpu_buffer_rsrc_t r, uint32_t off, const Sym<NV> &s) {
+  __builtin_amdgcn_raw_buffer_store_b32(s.l[0], r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(s.h[0], r, off + 32u, 0, 0);
+}
+
+template <int N, int NV, bool INV>
+__device__ __forceinline__ void xform_phase(const XformIO &io, bool first, bool last, const RsTab *__restrict__ tabs,
+                                         uint64_t ti, uint64_t size, uint64_t rmax, uint32_t dlo_log) {
+  const uint8_t *src = first ? io.src : io.work;
+  const uint64_t sps = first ? io.src_ps : io.work_ps, n_src = first ? io.n_src : size;
+  uint8_t *dst = last ? io.out : io.work;
+  const uint64_t dps = last ? io.out_ps : io.work_ps, n_dst = last ? io.n_out : size;
+  const bool sym = last && io.out_sym;
+  const uint64_t dlo = 1ull << dlo_log, span = static_cast<uint64_t>(N) << dlo_log;
+  for (uint64_t blk = 0; blk < size; blk += span) {
+    if (!INV && blk >= n_dst) break;  // FFT: a block past the stored outputs feeds nothing later
+    for (uint64_t lo = 0; lo < dlo; lo++) {
+      Sym<NV> s[N];
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dlo_log);
+        if (p < n_src) ldb(s[j], row_rsrc(src + p * sps), io.off);
+        else dev::zero(s[j]);
+      }
+      if constexpr (INV) ifft_sub<N, NV>(s, tabs, ti, size, rmax, blk, dlo_log);
+      else fft_sub<N, NV>(s, tabs, ti, size, rmax, blk, dlo_log);
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dlo_log);
+        if (p < n_dst) {
+          if (sym) dev::store_sym(dst + p * dps, io.off, s[j], io.contig);
+          else stb(row_rsrc(dst + p * dps), io.off, s[j]);
+        }
       }
     }
-    ti += 3 * (size / d4);
   }
-  if (d4 == 2) {
-    for (uint64_t r = 0; r < trunc; r += 2) {
-      const Tab t = dev::load_tab(tabs + ti + r / 2);
-      uint8_t *p0 = w + (pos + r) * ps, *p1 = p0 + ps;
-      Sym<NV> s0, s1;
-      ld(s0, p0);
-      ld(s1, p1);
-      dev::fft_bf(s0, s1, t);
-      st(p0, s0);
-      st(p1, s1);
+}
+
+// the whole transform of `size` points (a power of two) with truncation `trunc`
+template <int NV, bool INV>
+__device__ __forceinline__ void xform_ph(const XformIO &io, uint64_t size, uint64_t trunc, const RsTab *__restrict__ tabs) {
+  const uint32_t lg = log2_u64(size), n4 = lg / 2;
+  const bool r2 = lg & 1;
+  const uint64_t rmax = trunc < size ? trunc : size;
+  uint64_t ti = 0;
+  uint32_t layer = 0;  // radix-4 layers done (IFFT: from distance 1 up; FFT: from size/4 down)
+  bool r2_done = !r2, first = true;
+  do {
+    const uint32_t c = n4 - layer < 3 ? n4 - layer : 3;
+    const bool with_r2 = !r2_done && layer + c == n4 && c < 3;
+    const uint32_t n = (1u << (2 * c)) << (with_r2 ? 1 : 0);
+    const bool last = layer + c == n4 && (r2_done || with_r2);
+    // lowest distance of the phase (its position stride)
+    const uint32_t dlo_log = INV ? 2 * layer : (with_r2 || c == 0 ? 0 : lg - 2 * (layer + c));
+#define RS_XF_CASE(N_) \
+  case N_: xform_phase<N_, NV, INV>(io, first, last, tabs, ti, size, rmax, dlo_log); break;
+    switch (n) {
+      RS_XF_CASE(1) RS_XF_CASE(2) RS_XF_CASE(4) RS_XF_CASE(8) RS_XF_CASE(16) RS_XF_CASE(32) RS_XF_CASE(64)
     }
-  }
+#undef RS_XF_CASE
+    for (uint32_t l = layer; l < layer + c; l++) ti += INV ? 3 * (size >> (2 * l + 2)) : 3ull << (2 * l);
+    layer += c;
+    r2_done = r2_done || with_r2;
+    first = false;
+    if (c == 0) r2_done = true;  // the lone radix-2 phase (n == 2) just ran
+  } while (layer < n4 || !r2_done);
+}
+
+// in place on positions w + p*ps + off (the former layer-by-layer ifft_mem / fft_mem)
+template <int NV>
+__device__ __forceinline__ void ifft_mem(uint8_t *w, uint32_t off, uint64_t ps, uint64_t size, uint64_t trunc,
+                         const RsTab *__restrict__ tabs) {
+  const XformIO io{w, ps, size, w, ps, w, ps, size, false, false, off};
+  xform_ph<NV, true>(io, size, trunc, tabs);
+}
+template <int NV>
+__device__ __forceinline__ void fft_mem(uint8_t *w, uint32_t off, uint64_t ps, uint64_t size, uint64_t trunc,
+                        const RsTab *__restrict__ tabs) {
+  const XformIO io{w, ps, size, w, ps, w, ps, size, false, false, off};
+  xform_ph<NV, false>(io, size, trunc, tabs);
 }
 
 template <int NV>
@@ -731,17 +835,52 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
         else dev::zero(v);
         st(work + (j * C + p) * sb, v);
       }
-      ifft_mem<NV>(work, sb, j * C, C, t, a.tabs + static_cast<uint64_t>(j) * a.tabs_per_chunk);
+      ifft_mem<NV>(work - off + j * C * sb, off, sb, C, t, a.tabs + static_cast<uint64_t>(j) * a.tabs_per_chunk);
       if (j > 0)
         for (uint64_t p = 0; p < C; p++) xor_mem<NV>(work + p * sb, work + (j * C + p) * sb);
     }
-    fft_mem<NV>(work, sb, 0, C, a.m, a.tabs + static_cast<uint64_t>(a.n_chunks) * a.tabs_per_chunk);
+    fft_mem<NV>(work - off, off, sb, C, a.m, a.tabs + static_cast<uint64_t>(a.n_chunks) * a.tabs_per_chunk);
     uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
     for (uint64_t p = 0; p < a.m; p++) {
       Sym<NV> v;
       ld(v, work + p * sb);
       dev::store_sym(dst + p * sb, 0u, v, a.contig);
     }
+  }
+}
+
+// Formal derivative (root.zig:306-312): for i in [1, W), w[i - lowbit(i) + j] ^= w[i + j]
+// for j < lowbit(i). Reads lie at or above i and writes below it, so every read sees an
+// original value: out[p] = in[p] ^ XOR over clear bits b of p (b < log2 W) of in[p + 2^b].
+// Walked in 64-position blocks, ascending (every position a block reads lies above it, so
+// it is still original): the low 6 bits combine in VGPRs (ascending, the same argument),
+// the high bits add the partner blocks blk + 2^b. One independent load per term instead of
+// a dependent load-load-store chain per term.
+template <int NV>
+__device__ __forceinline__ void deriv_mem(uint8_t *w, uint32_t off, uint64_t ps, uint64_t W) {
+  const uint64_t B = W < 64 ? W : 64;
+  for (uint64_t blk = 0; blk < W; blk += B) {
+    Sym<NV> s[64];
+#pragma unroll
+    for (int l = 0; l < 64; l++)
+      if (static_cast<uint64_t>(l) < B) ldb(s[l], row_rsrc(w + (blk + l) * ps), off);
+#pragma unroll
+    for (int l = 0; l < 64; l++)
+#pragma unroll
+      for (int b = 0; b < 6; b++)
+        if (!((l >> b) & 1) && static_cast<uint64_t>(l + (1 << b)) < B) dev::xor_into(s[l], s[l + (1 << b)]);
+    for (uint64_t d = B; d < W; d <<= 1) {
+      if (blk & d) continue;
+#pragma unroll
+      for (int l = 0; l < 64; l++) {
+        Sym<NV> t;
+        ldb(t, row_rsrc(w + (blk + d + l) * ps), off);  // B == 64 here
+        dev::xor_into(s[l], t);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 64; l++)
+      if (static_cast<uint64_t>(l) < B) stb(row_rsrc(w + (blk + l) * ps), off, s[l]);
   }
 }
 
@@ -768,12 +907,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
       }
       st(work + p * sb, v);
     }
-    ifft_mem<NV>(work, sb, 0, W, a.trunc, a.tab_ifft);
-    for (uint64_t i = 1; i < W; i++) {
-      const uint64_t width = i & (~i + 1);
-      for (uint64_t j = 0; j < width; j++) xor_mem<NV>(work + (i - width + j) * sb, work + (i + j) * sb);
-    }
-    fft_mem<NV>(work, sb, 0, W, a.trunc_fft ? a.trunc_fft : a.trunc, a.tab_fft);
+    ifft_mem<NV>(work - off, off, sb, W, a.trunc, a.tab_ifft);
+    deriv_mem<NV>(work - off, off, sb, W);
+    fft_mem<NV>(work - off, off, sb, W, a.trunc_fft ? a.trunc_fft : a.trunc, a.tab_fft);
     uint8_t *out = a.out + s * a.out_stripe_stride + off;
     for (uint64_t p = 0; p < W; p++) {
       const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
@@ -828,44 +964,42 @@ __global__ __launch_bounds__(kBlock) void k_encode_low_reg(EncodeArgs a) {
   }
 }
 
-// Any C: each lane walks its column through a scratch [stripe][2C][sb] (coefficients
-// at [0, C), the current recovery chunk at [C, 2C)).
+// Any C: each lane walks its column through a scratch [stripe][(1 + n_chunks) C][sb]
+// (coefficients at [0, C), recovery chunk j's intermediate phases at [(1 + j) C, (2 + j) C)).
 __device__ __forceinline__ uint64_t ifft_tab_count_d(uint64_t size) {
   uint64_t n = 0, d = 1, d4 = 4;
   for (; d4 <= size; d = d4, d4 <<= 2) n += 3 * (size / d4);
   return n + (d < size ? 1 : 0);
 }
 
+// Stage 1 (blockIdx.z == 0 of k_encode_low_coef): coefficients = the originals -> IFFT ->
+// work[0, C) (no staging copy). Stage 2 (k_encode_low_generic, blockIdx.z = recovery chunk
+// j): coefficients -> FFT (intermediate phases in work[(1 + j) C, (2 + j) C)) -> parity
+// rows; the chunks run side by side (a lane's column walk is serial, so the grid's
+// chunk dimension is the parallelism left at small batches).
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_encode_low_coef(EncodeArgs a) {
+  uint32_t off;
+  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
+  const uint64_t sb = a.shard_bytes, C = a.chunk;
+  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+    uint8_t *work = a.scratch + s * (1 + a.n_chunks) * C * sb;
+    const XformIO ic{a.data + s * a.data_stripe_stride, sb, a.k, work, sb, work, sb, C, false, false, off};
+    xform_ph<NV, true>(ic, C, a.k, a.tabs);
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_low_generic(EncodeArgs a) {
   uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
-  const uint64_t sb = a.shard_bytes, C = a.chunk, TI = ifft_tab_count_d(C);
+  const uint64_t sb = a.shard_bytes, C = a.chunk, TI = ifft_tab_count_d(C), j = blockIdx.z;
+  const uint64_t t = a.m - j * C < C ? a.m - j * C : C;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    const uint8_t *src = a.data + s * a.data_stripe_stride + off;
-    uint8_t *work = a.scratch + s * 2 * C * sb + off;
-    for (uint64_t p = 0; p < C; p++) {
-      Sym<NV> v;
-      if (p < a.k) ld(v, src + p * sb);
-      else dev::zero(v);
-      st(work + p * sb, v);
-    }
-    ifft_mem<NV>(work, sb, 0, C, a.k, a.tabs);
-    uint8_t *dst = a.parity + s * a.parity_stripe_stride + off;
-    for (uint64_t j = 0; j < a.n_chunks; j++) {
-      const uint64_t t = a.m - j * C < C ? a.m - j * C : C;
-      for (uint64_t p = 0; p < C; p++) {
-        Sym<NV> v;
-        ld(v, work + p * sb);
-        st(work + (C + p) * sb, v);
-      }
-      fft_mem<NV>(work, sb, C, C, t, a.tabs + TI + j * a.tabs_per_chunk);
-      for (uint64_t p = 0; p < t; p++) {
-        Sym<NV> v;
-        ld(v, work + (C + p) * sb);
-        dev::store_sym(dst + (j * C + p) * sb, 0u, v, a.contig);
-      }
-    }
+    uint8_t *work = a.scratch + s * (1 + a.n_chunks) * C * sb;
+    uint8_t *dst = a.parity + s * a.parity_stripe_stride;
+    const XformIO fc{work, sb, C, work + (1 + j) * C * sb, sb, dst + j * C * sb, sb, t, true, a.contig, off};
+    xform_ph<NV, false>(fc, C, t, a.tabs + TI + j * a.tabs_per_chunk);
   }
 }
 
@@ -1490,8 +1624,8 @@ __global__ __launch_bounds__(kBlock) void k_engine_transform(uint8_t *work, uint
                                                              uint64_t trunc, const RsTab *tabs, int inverse) {
   uint32_t off;
   if (!lane_offset<1>(sb, false, off)) return;
-  if (inverse) ifft_mem<1>(work + off, sb, pos, size, trunc, tabs);
-  else fft_mem<1>(work + off, sb, pos, size, trunc, tabs);
+  if (inverse) ifft_mem<1>(work + pos * sb, off, sb, size, trunc, tabs);
+  else fft_mem<1>(work + pos * sb, off, sb, size, trunc, tabs);
 }
 
 __global__ __launch_bounds__(kBlock) void k_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab) {
@@ -1620,7 +1754,12 @@ KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv) {
 
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
   if (kc.variant == Variant::kGeneric) {
-    hipLaunchKernelGGL(k_encode_low_generic<1>, grid_for(a.shard_bytes, 1, a.n_stripes), dim3(kBlock), 0, s, a);
+    // a.scratch: (1 + n_chunks) C positions per stripe (low_encode)
+    const dim3 g = grid_for(a.shard_bytes, 1, a.n_stripes);
+    hipLaunchKernelGGL(k_encode_low_coef<1>, g, dim3(kBlock), 0, s, a);
+    if (hipError_t e = hipGetLastError()) return e;
+    if (a.n_chunks > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_encode_low_generic<1>, dim3(g.x, g.y, static_cast<uint32_t>(a.n_chunks)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
   }
   for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {

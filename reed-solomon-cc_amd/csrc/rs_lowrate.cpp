@@ -260,7 +260,8 @@ int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const u
     HIP_TRY(launch_encode_low(kc, a, s));
     return RS_OK;
   }
-  return in_scratch_slices(n, 2ull * p->C * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
+  // coefficients + one intermediate region per recovery chunk (the chunks' FFTs run in parallel)
+  return in_scratch_slices(n, (1ull + p->n_chunks) * p->C * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
     EncodeArgs b = a;
     b.data += s0 * ostride;
     b.parity += s0 * rstride;

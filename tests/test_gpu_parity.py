@@ -121,6 +121,10 @@ def test_exhaustive_rs5_5_roundtrip():
     (4, 0, 4, 4, 4), (4, 0, 4, 3, 8), (8, 4, 4, 2, 12), (16, 0, 16, 14, 0), (16, 0, 16, 16, 0),
     (8, 0, 8, 8, 0), (8, 0, 8, 5, 16), (2, 0, 2, 2, 2), (32, 0, 32, 20, 0), (64, 0, 64, 64, 64),
     (512, 0, 512, 456, 0), (6, 2, 4, 4, 300), (2, 0, 2, 1, 1000),
+    # the phased column walk (rs_kernels.hip xform_ph): a lone radix-2 phase (128), two
+    # and three phases, truncation inside and at the phase blocks, an offset window
+    (128, 0, 128, 100, 0), (1024, 0, 1024, 1000, 5), (2048, 0, 2048, 2048, 0),
+    (4096, 0, 4096, 3000, 0), (8192, 0, 8192, 5000, 7), (8192, 0, 8192, 64, 0), (260, 4, 256, 200, 3),
 ])
 def test_engine_fft_ifft_vs_oracle(oracle, flags, case):
     count, pos, size, trunc, sd = case

@@ -39,6 +39,8 @@ def main():
         erase = list(range(first, first + cnt * step, step))
     else:
         erase = [int(x) for x in args.erase.split(",") if x]
+    if any(not 0 <= i < k for i in erase):  # erased data shards only (data[:, erase] below)
+        raise SystemExit(f"--erase names shards outside [0, {k}): {erase}")
     e = len(erase)
     present = [0 if i in erase else 1 for i in range(k)] + [1] * m
     dev = torch.device("cuda:0")
