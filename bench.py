@@ -150,14 +150,34 @@ def _cpu_model():
     return "unknown"
 
 
+def _time_calls(fn, reps):
+    """HIP events around `reps` calls (after one untimed call) and the kernels every call
+    launched (rs_last_kernels: what ran, not what a name query predicts)."""
+    fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ran = set()
+    a.record()
+    for _ in range(reps):
+        fn()
+        ran.add(";".join(R.last_kernels()))
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps, sorted(ran)
+
+
 def c4_leg(dev, reps, n=512):
     """BASELINE configs[4] on the GPU, outside the timed region (rank 0, N=1): RS(200,55)
     256 KiB x n (512 stripes, 25 GiB of data) encode and reconstruct of 55
-    erased data shards (every third from 1), HIP events over `reps` calls after a warm-up
-    that includes the kernels' hipRTC compiles (background compiles joined with net_wait).
-    Then a cold pattern (every third from 2, never seen by the process): its first calls
-    timed without net_wait, as a repair service meeting a new pattern runs them. Restored
-    shards are checked against the data."""
+    erased data shards (every third from 1), HIP events over `reps` calls.
+
+    reconstruct: the pattern's steady state after rs_reconstruct_warm (its full plan and
+    every kernel it launches compiled and loaded); reconstruct_fused / reconstruct_network:
+    the two forms a wide-code pattern can run (RS_AMD_FDEC=1: the fused FFT reconstruct;
+    RS_AMD_FDEC=0: syndromes on the FFT kernel + the pattern's e x e network), each warmed
+    the same way. Every entry names the kernels its calls actually launched. Then a cold
+    pattern (every third from 2, never seen by the process): its first calls without any
+    warm-up, as a repair service meeting a new pattern runs them. Restored shards are
+    checked against the data."""
     k, m, sb = 200, 55, 256 << 10
     lost = list(range(1, k, 3))[:m]
     present = [0 if i in lost else 1 for i in range(k)] + [1] * m
@@ -166,29 +186,37 @@ def c4_leg(dev, reps, n=512):
     data = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8, device=dev, generator=g)
     par = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
     out = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
-    for _ in range(2):
-        R.encode_batch_dev(k, m, data, par)
-        R.reconstruct_batch_dev(k, m, present, data, par, out)
+    R.encode_batch_dev(k, m, data, par)
     torch.cuda.synchronize()
     R.net_wait()
     res = {"workload": f"RS(200,55) 256 KiB shards x {n} stripes; reconstruct: 55 erased data shards "
                        "(every third from 1)"}
-    for name, fn, alg in (("encode", lambda: R.encode_batch_dev(k, m, data, par), (k + m) * sb * n),
-                          ("reconstruct", lambda: R.reconstruct_batch_dev(k, m, present, data, par, out),
-                           (k + m) * sb * n)):
-        fn()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(reps):
-            fn()
-        b.record()
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / reps
-        res[name] = {"ms": round(ms, 3), "GiBps": round(k * sb * n / (ms * 1e-3) / 2**30, 1),
-                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "kernel": (R.encode_kernel_name(k, m, sb) if name == "encode"
-                                else R.reconstruct_kernel_name(k, m, sb, present))}
-    res["verified"] = bool(torch.equal(out, data[:, lost]))
+    alg = (k + m) * sb * n
+    ok = True
+
+    def entry(ms, ran):
+        return {"ms": round(ms, 3), "GiBps": round(k * sb * n / (ms * 1e-3) / 2**30, 1),
+                "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "kernels": ran}
+
+    res["encode"] = entry(*_time_calls(lambda: R.encode_batch_dev(k, m, data, par), reps))
+    rec = lambda: R.reconstruct_batch_dev(k, m, present, data, par, out)  # noqa: E731
+    prev = os.environ.get("RS_AMD_FDEC")
+    try:
+        for name, fdec in (("reconstruct", prev), ("reconstruct_fused", "1"), ("reconstruct_network", "0")):
+            if fdec is None:
+                os.environ.pop("RS_AMD_FDEC", None)
+            else:
+                os.environ["RS_AMD_FDEC"] = fdec
+            R.reconstruct_warm(k, m, sb, present)
+            out.zero_()
+            res[name] = entry(*_time_calls(rec, reps))
+            ok = ok and bool(torch.equal(out, data[:, lost]))
+    finally:
+        if prev is None:
+            os.environ.pop("RS_AMD_FDEC", None)
+        else:
+            os.environ["RS_AMD_FDEC"] = prev
+    res["verified"] = ok
     # cold pattern: first calls of an erasure pattern whose kernels are not compiled
     lost_c = list(range(2, k, 3))[:m]
     present_c = [0 if i in lost_c else 1 for i in range(k)] + [1] * m
@@ -198,11 +226,13 @@ def c4_leg(dev, reps, n=512):
         t0 = time.perf_counter()
         a.record()
         R.reconstruct_batch_dev(k, m, present_c, data, par, out)
+        ran = R.last_kernels()
         b.record()
         torch.cuda.synchronize()
-        calls.append({"wall_ms": round((time.perf_counter() - t0) * 1e3, 3), "gpu_ms": round(a.elapsed_time(b), 3)})
+        calls.append({"wall_ms": round((time.perf_counter() - t0) * 1e3, 3), "gpu_ms": round(a.elapsed_time(b), 3),
+                      "kernels": ran})
     res["reconstruct_cold"] = {"calls": calls, "pattern": "55 erased data shards, every third from 2",
-                               "note": "first calls of a new pattern, no net_wait (plan build included in wall_ms)",
+                               "note": "first calls of a new pattern, no warm-up (plan build included in wall_ms)",
                                "verified": bool(torch.equal(out, data[:, lost_c]))}
     del data, par, out
     torch.cuda.empty_cache()
@@ -248,19 +278,25 @@ def main():
     restored = torch.empty((n, e, sb), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream()
 
+    launched = {"encode": set(), "reconstruct": set()}  # rs_last_kernels after every call
+
     def step(ev=None):
         if ev:
             ev[0].record(stream)
         R.encode_batch_dev(k, m, data, parity, stream=stream)
+        launched["encode"].add(";".join(R.last_kernels()))
         if ev:
             ev[1].record(stream)
         R.reconstruct_batch_dev(k, m, present, data, parity, restored, stream=stream)
+        launched["reconstruct"].add(";".join(R.last_kernels()))
         if ev:
             ev[2].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    for v in launched.values():
+        v.clear()  # report what the timed steps ran
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -305,7 +341,8 @@ def main():
                     "per_kernel": {kk: {"kernel": v[2], "avg_ms": round(v[0], 4),
                                         "achieved_GBps": round(v[1] / (v[0] * 1e-3) / 1e9, 1),
                                         "frac": round(v[1] / (v[0] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                                        "data_GiBps": round(data_bytes / (v[0] * 1e-3) / 2**30, 1)}
+                                        "data_GiBps": round(data_bytes / (v[0] * 1e-3) / 2**30, 1),
+                                        "launched": sorted(launched[kk])}
                                    for kk, v in kinds.items()}}
         cpu = None  # host-core baseline: rank 0 at N=1 only (the driver's N>1 runs skip it)
         if args.cpu_seconds > 0 and world == 1:

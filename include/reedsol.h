@@ -194,11 +194,30 @@ const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_c
                                     uint32_t max_e, uint32_t flags);
 
 /* Large reconstruct network maps (the e x e syndrome map of wide codes, e.g. RS(200,55)
- * losing 55 data shards: ~16-36 s of hipRTC) compile in a background thread; until they are
- * ready the plan runs its table kernel (same bytes). rs_net_wait blocks until no such
- * compile is running — a service can warm a pattern with one call + rs_net_wait.
- * RS_AMD_JIT_SYNC=1 compiles them in the calling thread instead. Returns RS_OK. */
+ * losing 55 data shards: ~16-36 s of hipRTC) compile in a background thread. A wide-code
+ * pattern's first calls run the fused FFT reconstruct (rs_fft_decode_*, the pattern as
+ * data); where a network beats it, the pattern's second call queues the full plan's build
+ * and, behind it, the network's compile on the background worker, and the calls run the
+ * fused kernel until the network is loaded. rs_net_wait blocks until the worker is idle
+ * (no plan build or compile queued or running): after two calls + rs_net_wait the next
+ * call runs the pattern's steady-state kernel. RS_AMD_JIT_SYNC=1 compiles in the calling
+ * thread instead. Returns RS_OK. */
 int rs_net_wait(void);
+
+/* Drive one erasure pattern of rs_reconstruct_batch_dev (same arguments) to its steady
+ * state without running a batch: build its full plan and compile and load every kernel
+ * its calls will launch, blocking until done. The next call runs the steady-state kernel
+ * (check with rs_last_kernels). */
+int rs_reconstruct_warm(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, const uint8_t *present,
+                        uint32_t flags);
+
+/* The kernels the calling thread's most recent compute call (the *_dev, *_host, one-shot,
+ * Encoder/Decoder and engine entry points) launched, in launch order, ';'-separated,
+ * consecutive repeats collapsed: hipRTC kernels by symbol (rs_net_encode_i10_o4_<hash>,
+ * rs_fft_decode_k200_m55_..., the names rocprofv3 reports), precompiled ones by their
+ * rs_*_kernel_name form (encode_reg_w4_nv4, k_erasure_logs, ...). Host batches launch on
+ * worker threads and are recorded there, not here. Valid until the thread's next call. */
+const char *rs_last_kernels(void);
 
 /* hipRTC activity of this process: kernels compiled, code objects found in the on-disk
  * cache ($RS_AMD_CACHE_DIR, else $XDG_CACHE_HOME/rs_amd or ~/.cache/rs_amd; empty = off),

@@ -87,6 +87,7 @@ extern "C" {
 int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, const void *d_original,
                         uint64_t orig_stride, void *d_recovery, uint64_t rec_stride, uint32_t flags,
                         rs_stream_t stream) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
     int st = check_codec(k, m, sb);
@@ -178,6 +179,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
                              const void *d_original, uint64_t orig_stride, const void *d_recovery,
                              uint64_t rec_stride, void *d_restored, uint64_t out_stride, uint32_t flags,
                              rs_stream_t stream) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
     int st = check_codec(k, m, sb);
@@ -385,6 +387,50 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       }
     }
     HIP_TRY(hipFreeAsync(scratch, s));
+    return RS_OK;
+  });
+}
+
+// Drive one erasure pattern to its steady state: the plan the pattern's later calls use
+// (a lite plan's background upgrade included) and every kernel they launch, compiled and
+// loaded, blocking until done. The same sequence a stream of calls would go through
+// (get_decode_plan's first and second use), without waiting for those calls.
+int rs_reconstruct_warm(uint64_t k, uint64_t m, size_t sb, const uint8_t *present, uint32_t flags) {
+  return guarded([&]() -> int {
+    if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+    int st = check_codec(k, m, sb);
+    if (st) return st;
+    uint64_t have = 0, e = 0;
+    for (uint64_t i = 0; i < k + m; i++) have += present[i] != 0;
+    for (uint64_t i = 0; i < k; i++) e += present[i] == 0;
+    if (have < k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+    if (e == 0) return RS_OK;
+    const uint64_t psb = (sb + 63) / 64 * 64;  // tails run on padded shards
+    int dev;
+    if ((st = current_device(&dev))) return st;
+    if (is_low_rate(k, m)) return low_warm(dev, k, m, psb, present);
+    std::shared_ptr<DecodePlan> plan;
+    if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan))) return st;
+    if (plan->lite) {  // the second use decides (and queues) the upgrade; wait for it
+      if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan))) return st;
+      jit::wait_pending();
+      if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan))) return st;
+    }
+    const fftnet::Spec *fs = nullptr;
+    if (plan->inv_fft) (void)fft_kernel(*plan->inv_fft, psb, &fs);
+    if (plan->net) queue_net(*plan->net, psb);
+    if (plan->fdec_blk && fdec_supports(k, m, psb, flags)) {
+      std::shared_ptr<WpsSlot> ws;
+      wps_slot(dev, k, m, 0, ws);
+      (void)fft_kernel(*ws->dec, psb, &fs);
+    }
+    if (plan->syndrome && plan->syn_blk) {
+      std::shared_ptr<WpsSlot> ws;
+      wps_slot(dev, k, m, 0, ws);
+      (void)fft_kernel(*ws->fft, psb, &fs);
+      (void)wps_solve_kernel(*ws);
+    }
+    jit::wait_pending();
     return RS_OK;
   });
 }

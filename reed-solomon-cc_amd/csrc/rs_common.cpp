@@ -22,6 +22,34 @@ int hip_fail(hipError_t e, const char *what) {
 
 const char *last_error() { return t_last_error.c_str(); }
 
+}  // namespace host
+
+// ---------------------------------------------------------- launch record
+namespace {
+thread_local std::string t_trace;       // names joined by ';' in launch order
+thread_local std::string t_trace_last;  // collapse repeats (slices of one batch)
+thread_local int t_trace_depth = 0;
+}  // namespace
+
+void trace_launch(const char *name) {
+  if (!name || t_trace_last == name) return;
+  t_trace_last = name;
+  if (!t_trace.empty()) t_trace.push_back(';');
+  t_trace += name;
+}
+
+TraceScope::TraceScope() {
+  if (t_trace_depth++ == 0) {
+    t_trace.clear();
+    t_trace_last.clear();
+  }
+}
+TraceScope::~TraceScope() { t_trace_depth--; }
+
+const char *trace_text() { return t_trace.c_str(); }
+
+namespace host {
+
 // ---------------------------------------------------------------- devices
 std::mutex g_dev_mu;
 std::map<int, int> g_dev_ok;  // device -> RS_OK / RS_ERR_NO_DEVICE
@@ -146,6 +174,14 @@ const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb) {
   return k;
 }
 
+void queue_net(NetSlot &slot, uint64_t sb) {
+  {
+    std::lock_guard<std::mutex> lk(slot.mu);
+    slot.uses = std::max(slot.uses, async_after());  // a warmed pattern is not a one-off
+  }
+  (void)net_kernel(slot, sb);
+}
+
 std::mutex g_plan_mu;
 
 namespace {
@@ -174,11 +210,21 @@ int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &o
   return RS_OK;
 }
 
+// Plan uploads go through a private non-blocking stream per (thread, device): a
+// synchronous hipMemcpy runs on the null stream, which orders itself against every
+// blocking stream of the device — an upload from the background worker (a plan upgrade)
+// would then wait for the caller's in-flight batches and delay its next launches.
+// (The streams are never destroyed: a destructor at thread exit could run after the HIP
+// runtime's teardown)
 int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out) {
+  thread_local std::map<int, hipStream_t> streams;
   auto b = std::make_shared<DevBuf>();
   b->dev = dev;
   HIP_TRY(hipMalloc(&b->p, std::max<size_t>(bytes, 16)));
-  HIP_TRY(hipMemcpy(b->p, host, bytes, hipMemcpyHostToDevice));
+  hipStream_t &st = streams[dev];
+  if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIP_TRY(hipMemcpyAsync(b->p, host, bytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
   out = b;
   return RS_OK;
 }
@@ -216,6 +262,8 @@ const char *rs_status_name(int s) {
 }
 
 const char *rs_last_error(void) { return last_error(); }
+
+const char *rs_last_kernels(void) { return trace_text(); }
 
 int rs_use_high_rate(uint64_t k, uint64_t m) { return use_high_rate(k, m); }
 

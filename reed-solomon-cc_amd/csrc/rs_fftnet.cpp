@@ -12,6 +12,7 @@
 
 #include "reedsol.h"
 #include "rs_gf.hpp"
+#include "rs_internal.hpp"
 
 namespace rs {
 namespace fftnet {
@@ -1297,6 +1298,7 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
   const uint32_t *dm = dmask;
   uint32_t dmw = shared_mask ? 0u : dmask_words;  // the kernel's per-stripe mask stride
   void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st, &dm, &dmw};
+  trace_launch(kn.name.c_str());
   return hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(grid), 1, 1, (C / 8) * 64, 1, 1, 0, st, args, nullptr);
 }
 

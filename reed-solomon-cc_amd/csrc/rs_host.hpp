@@ -62,6 +62,15 @@ int current_device(int *dev);  // RS_ERR_NO_DEVICE unless the current device is 
 // root.zig:397-415: 1 high rate, 0 low rate, -status on invalid counts
 int use_high_rate(uint64_t original, uint64_t recovery);
 inline bool is_low_rate(uint64_t k, uint64_t m) { return use_high_rate(k, m) == 0; }
+// The reconstruct as written reads every present shard and is no decoder of the parity the
+// encode wrote: under D1 (Generic.zig:283, the multiply) and under D2 when it drops a chunk
+// (root.zig:151, k > chunk and k % chunk == 0: the parity ignores those shards). Such
+// reconstructs run on maps of all present shards (no trimming to k inputs, no syndromes,
+// no solve), so they stay bit-exact with the reference on any set of present shards.
+inline bool literal_decode(uint64_t k, uint64_t m, uint32_t flags) {
+  const uint64_t C = ceil_pow2(m);
+  return (flags & RS_FLAG_QUIRK_D1) || ((flags & RS_FLAG_QUIRK_D2) && k > C && k % C == 0);
+}
 // Encoder.init / Decoder.init checks (root.zig:100-103, 198-201)
 int check_codec(uint64_t k, uint64_t m, size_t shard_bytes);
 // widest per-lane access (4, 2, 1 dword pairs) the alignment of every value allows; 0 = none
@@ -109,6 +118,9 @@ bool fft_enabled();
 const jit::Kernel *fft_kernel(FftSlot &slot, uint64_t sb, const fftnet::Spec **used);
 // The slot's network kernel (compiled on first use; nullptr: table kernels)
 const jit::Kernel *net_kernel(NetSlot &slot, uint64_t sb);
+// Start the slot's compile now (an async slot: queued on the background worker, whatever
+// its use count), e.g. when a plan upgrade or rs_reconstruct_warm knows it will be used.
+void queue_net(NetSlot &slot, uint64_t sb);
 
 struct EncodePlan {
   std::shared_ptr<DevBuf> buf;
@@ -241,6 +253,8 @@ int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const u
 int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *present,
                     const uint8_t *orig, uint64_t ostride, const uint8_t *rec, uint64_t rstride, uint8_t *out,
                     uint64_t outstride, uint32_t flags, int max_nv, hipStream_t s);
+// rs_reconstruct_warm for a low-rate pattern: its plan, and its network compiled
+int low_warm(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present);
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb);
 const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e);
 int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);

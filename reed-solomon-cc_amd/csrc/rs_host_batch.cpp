@@ -105,6 +105,7 @@ extern "C" {
 
 int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const void *h_orig, uint64_t orig_stride,
                          void *h_rec, uint64_t rec_stride, uint32_t flags) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (k == 0) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "original_count == 0");
     int st = check_codec(k, m, sb);
@@ -143,6 +144,7 @@ int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const vo
 int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const uint8_t *present,
                               const void *h_orig, uint64_t orig_stride, const void *h_rec, uint64_t rec_stride,
                               void *h_out, uint64_t out_stride, uint32_t flags) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
     int st = check_codec(k, m, sb);
@@ -237,6 +239,7 @@ extern "C" {
 
 int rs_encode_batch_host_multi(uint64_t k, uint64_t m, size_t sb, uint64_t n, const void *h_orig, uint64_t orig_stride,
                                void *h_rec, uint64_t rec_stride, uint32_t flags, const int *devices, int n_devices) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (orig_stride == 0) orig_stride = k * sb;
     if (rec_stride == 0) rec_stride = m * sb;
@@ -251,6 +254,7 @@ int rs_reconstruct_batch_host_multi(uint64_t k, uint64_t m, size_t sb, uint64_t 
                                     const void *h_orig, uint64_t orig_stride, const void *h_rec, uint64_t rec_stride,
                                     void *h_out, uint64_t out_stride, uint32_t flags, const int *devices,
                                     int n_devices) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
     uint64_t e = 0;

@@ -8,6 +8,17 @@
 
 namespace rs {
 
+// Launch record (rs_last_kernels): every launcher below and every hipRTC launch notes
+// the kernel it launched for the calling thread; a C-ABI compute entry point clears the
+// record when it starts (TraceScope, outermost call only), so after the call the record
+// lists what that call actually ran, in launch order (repeats collapsed).
+void trace_launch(const char *name);
+struct TraceScope {
+  TraceScope();
+  ~TraceScope();
+};
+const char *trace_text();
+
 // Encode: data [stripe][k][sb] -> parity [stripe][m][sb].
 // Table block: n_chunks x ifft_tab_count(chunk) (chunk j has skew_delta (j+1)*chunk),
 // then fft_tab_count(chunk) (skew_delta 0).

@@ -1058,6 +1058,7 @@ hipError_t launch(const Kernel &k, const uint8_t *buf0, uint64_t stride0, const 
                   const uint8_t *buf2, uint64_t stride2) {
   if (n_stripes == 0) return hipSuccess;
   if (k.pieces > 1 && shard_bytes * k.pieces != kUnitBytes) return hipErrorInvalidValue;  // wrong kernel for sb
+  trace_launch(k.name.c_str());
   if (k.shared) {  // one workgroup of n_tiles waves per 4 KiB unit (generate_shared)
     const uint64_t units = shard_bytes / kUnitBytes;
     if (units == 0 || units > 0x7fffffffull || shard_bytes % kUnitBytes) return hipErrorInvalidValue;

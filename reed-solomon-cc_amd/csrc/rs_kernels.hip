@@ -1555,6 +1555,8 @@ hipError_t launch_pattern_matrix_impl(const uint8_t *d_present, uint64_t present
                                       int32_t *nout, hipStream_t s) {
   const uint64_t threads = n * k * 16;
   const dim3 grid(static_cast<uint32_t>((threads + 255) / 256));
+  trace_launch("k_pattern_images");
+  trace_launch("k_pattern_mtabs");
   switch (W) {
 #define RS_PIMG(W_)                                                                                                   \
   case W_:                                                                                                            \
@@ -1577,6 +1579,8 @@ hipError_t launch_pattern_plan_impl(const uint8_t *d_present, uint64_t present_s
                                     uint32_t C, uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
                                     const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
                                     RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
+  trace_launch("k_erasure_logs");
+  trace_launch("k_pattern_tables");
   for (uint64_t s0 = 0; s0 < n; s0 += 65535) {
     const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
     hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, d_present + s0 * present_stride,
@@ -1753,6 +1757,7 @@ KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv) {
   }
 
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
+  trace_launch(kc.name);
   if (kc.variant == Variant::kGeneric) {
     // a.scratch: (1 + n_chunks) C positions per stripe (low_encode)
     const dim3 g = grid_for(a.shard_bytes, 1, a.n_stripes);
@@ -1834,6 +1839,7 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
 // kernel: a loop lets the compiler hoist every per-stripe-invariant uniform value
 // into SGPRs and spill them), so batches are launched in slices of <= 65535 stripes.
 hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
+  trace_launch(kc.name);
   if (kc.variant == Variant::kGeneric) return launch_encode_one(kc, a, s);
   for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {
     EncodeArgs b = a;
@@ -1847,6 +1853,7 @@ hipError_t launch_encode(const KernelChoice &kc, const EncodeArgs &a, hipStream_
 }
 
 hipError_t launch_decode(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
+  trace_launch(kc.name);
   if (kc.variant == Variant::kGeneric) return launch_decode_one(kc, a, s);
   for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {
     DecodeArgs b = a;
@@ -1944,6 +1951,7 @@ hipError_t launch_psyn_plan(const uint8_t *present, uint64_t present_stride, uin
                             uint32_t *plan, uint32_t plan_dw, int32_t *status, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (k > 256 || m > kPsynMaxM || max_out > m || plan_dw < (k + 31) / 32 + 2 + m * max_out) return hipErrorInvalidValue;
+  trace_launch("k_psyn_plan");
   hipLaunchKernelGGL(k_psyn_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present, present_stride,
                      k, m, max_out, max_e, n, G, d_exp, d_log, plan, plan_dw, status);
   return hipGetLastError();
@@ -1960,6 +1968,7 @@ hipError_t launch_wps_plan(const uint8_t *present, uint64_t present_stride, uint
   const uint32_t cs = wps_coef_stride(max_e);
   if (m > kWpsMaxM || dmw < 2 || plan_dw < dmw + 2 + kWpsMaxM + kWpsMaxM * cs || (dmw - 2) * 32 < k)
     return hipErrorInvalidValue;
+  trace_launch(cs == kWpsMaxOut ? "k_wps_plan" : "k_wps_plan_wave");
   if (cs == kWpsMaxOut) {
     hipLaunchKernelGGL(k_wps_plan, dim3(static_cast<uint32_t>((n + 63) / 64)), dim3(64), 0, s, present,
                        present_stride, k, m, max_e, n, G, d_exp, d_log, plan, plan_dw, dmw, status);
@@ -2045,6 +2054,9 @@ hipError_t launch_fdec_plan(const uint8_t *present, uint64_t present_stride, uin
                             hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (W / C > 32 || mko < dwm + 3 + k || words < mko + 128 * (m + k)) return hipErrorInvalidValue;
+  trace_launch("k_trim_present");
+  trace_launch("k_erasure_logs");
+  trace_launch("k_fdec_block");
   hipLaunchKernelGGL(k_trim_present, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, present,
                      present_stride, k, m, n, trimmed);
   hipError_t e = hipGetLastError();
@@ -2063,6 +2075,7 @@ hipError_t launch_fdec_plan(const uint8_t *present, uint64_t present_stride, uin
 
 hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, uint32_t k, uint32_t m, uint64_t n,
                                uint8_t *out, hipStream_t s) {
+  trace_launch("k_trim_present");
   hipLaunchKernelGGL(k_trim_present, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, present,
                      present_stride, k, m, n, out);
   return hipGetLastError();
@@ -2071,6 +2084,7 @@ hipError_t launch_trim_present(const uint8_t *present, uint64_t present_stride, 
 hipError_t launch_tail_pack(const uint8_t *src, uint64_t src_stripe_stride, uint8_t *dst, uint64_t dst_stripe_stride,
                             uint64_t sb, uint64_t n, bool unpack, hipStream_t s) {
   if (sb % 64 == 0 || n == 0) return hipSuccess;
+  trace_launch("k_tail_pack");
   const uint64_t blocks = (n * 64 + 255) / 256;
   hipLaunchKernelGGL(k_tail_pack, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, src, src_stripe_stride, dst,
                      dst_stripe_stride, sb, n, unpack ? 1 : 0);
@@ -2080,6 +2094,7 @@ hipError_t launch_tail_pack(const uint8_t *src, uint64_t src_stripe_stride, uint
 hipError_t launch_engine_fft(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
                              const RsTab *tabs, bool inverse, hipStream_t s) {
   const dim3 grid = grid_for(sb, 1, 1);
+  trace_launch("k_engine_transform");
   hipLaunchKernelGGL(k_engine_transform, grid, dim3(kBlock), 0, s, work, sb, pos, size, trunc, tabs,
                      inverse ? 1 : 0);
   return hipGetLastError();
@@ -2087,6 +2102,7 @@ hipError_t launch_engine_fft(uint8_t *work, uint64_t sb, uint64_t pos, uint64_t 
 
 hipError_t launch_mul_scalar(uint8_t *chunks, uint64_t bytes, const RsTab *tab, hipStream_t s) {
   const dim3 grid = grid_for(bytes, 1, 1);
+  trace_launch("k_mul_scalar");
   hipLaunchKernelGGL(k_mul_scalar, grid, dim3(kBlock), 0, s, chunks, bytes, tab);
   return hipGetLastError();
 }

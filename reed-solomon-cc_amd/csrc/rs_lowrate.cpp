@@ -322,6 +322,16 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
   });
 }
 
+int low_warm(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present) {
+  std::shared_ptr<LowDecodePlan> p;
+  if (int st = get_low_decode_plan(dev, k, m, sb, present, p)) return st;
+  if (p->net) {
+    queue_net(*p->net, sb);
+    jit::wait_pending();
+  }
+  return RS_OK;
+}
+
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb) {
   if (map_net_ok(k, m, sb)) return net_name("encode_low", k, m);
   return choose_encode_low(ceil_pow2(k), sb, 4).name;

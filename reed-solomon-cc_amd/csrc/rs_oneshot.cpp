@@ -92,6 +92,7 @@ inline size_t align256(size_t x) { return (x + 255) & ~static_cast<size_t>(255);
 extern "C" {
 
 int rs_encode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, uint8_t *const *recovery_out) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (k == 0 || !original) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "no original shards");  // root.zig:20
     int st = check_codec(k, m, sb);
@@ -118,6 +119,7 @@ int rs_encode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original,
 
 int rs_decode(uint64_t k, uint64_t m, size_t sb, const uint8_t *const *original, const uint8_t *const *recovery,
               uint8_t *const *restored_out) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!original || !recovery || !restored_out) return fail(RS_ERR_INVALID_ARGUMENT, "NULL array");
     uint64_t orig_present = 0, rec_present = 0;
@@ -205,6 +207,7 @@ int rs_encoder_add_original_shard(rs_encoder *e, const uint8_t *shard, size_t le
 }
 
 int rs_encoder_encode(rs_encoder *e, const uint8_t **recovery_out) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!e) return fail(RS_ERR_INVALID_ARGUMENT, "NULL encoder");
     if (e->received != e->k) return fail(RS_ERR_TOO_FEW_ORIGINAL_SHARDS, "too few original shards");  // root.zig:139
@@ -295,6 +298,7 @@ int rs_decoder_add_recovery_shard(rs_decoder *d, uint64_t index, const uint8_t *
 
 // root.zig:268-335; restored_out[i] points at the original (supplied or restored)
 int rs_decoder_decode(rs_decoder *d, const uint8_t **restored_out) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!d) return fail(RS_ERR_INVALID_ARGUMENT, "NULL decoder");
     if (d->orig_received + d->rec_received < d->k) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "not enough shards");
@@ -339,6 +343,7 @@ static int engine_transform(uint8_t *shards, uint64_t count, size_t sb, uint64_t
 
 int rs_engine_fft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
                   uint64_t sd, uint32_t flags) {
+  TraceScope ts;
   return guarded([&]() -> int {
     return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, false);
   });
@@ -346,12 +351,14 @@ int rs_engine_fft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint
 
 int rs_engine_ifft(uint8_t *shards, uint64_t count, size_t sb, uint64_t pos, uint64_t size, uint64_t trunc,
                    uint64_t sd, uint32_t flags) {
+  TraceScope ts;
   return guarded([&]() -> int {
     return engine_transform(shards, count, sb, pos, size, trunc, sd, flags, true);
   });
 }
 
 int rs_engine_mul_scalar(uint8_t *chunks, size_t bytes, uint16_t log_m, uint32_t flags) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!chunks) return fail(RS_ERR_INVALID_ARGUMENT, "NULL chunks");
     if (bytes == 0 || bytes % 64) return fail(RS_ERR_INVALID_SHARD_SIZE, "bytes must be a multiple of 64");
@@ -370,6 +377,7 @@ int rs_engine_mul_scalar(uint8_t *chunks, size_t bytes, uint16_t log_m, uint32_t
 }
 
 int rs_engine_eval_poly(uint16_t *erasures, uint64_t trunc) {
+  TraceScope ts;
   return guarded([&]() -> int {
     if (!erasures) return fail(RS_ERR_INVALID_ARGUMENT, "NULL erasures");
     if (trunc > kOrder) return fail(RS_ERR_INVALID_ARGUMENT, "truncated_size > 65536");

@@ -201,7 +201,7 @@ const char *rs_patterns_kernel_name(uint64_t k, uint64_t m, size_t sb, uint32_t 
     const char *pm = std::getenv("RS_AMD_PATTERNS");
     const uint64_t W = ceil_pow2(ceil_pow2(m) + k);
     const bool matrix =
-        !(flags & RS_FLAG_QUIRK_D1) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
+        !literal_decode(k, m, flags) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
     name = matrix ? "pattern_matrix" : "pattern_fft";
   }
   return name.c_str();
@@ -212,6 +212,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
                                       uint64_t orig_stride, const void *d_recovery, uint64_t rec_stride,
                                       void *d_restored, uint64_t out_stride, int32_t *d_status, uint32_t flags,
                                       rs_stream_t stream) {
+  TraceScope ts;
   return guarded([&]() -> int {
     int st = check_codec(k, m, sb);
     if (st == RS_OK && is_low_rate(k, m))
@@ -377,7 +378,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     // matrix path (below): corrected multiply, W <= 32, max_e <= 8
     const char *pm = std::getenv("RS_AMD_PATTERNS");
     const bool use_matrix =
-        !(flags & RS_FLAG_QUIRK_D1) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
+        !literal_decode(k, m, flags) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
     // per-stripe plan: logs u16 | pre RsTab | post RsTab | src i32 | dst i32 (W entries each)
     //                  [| trimmed present rows, matrix path]
     const uint64_t per = W * (2 + 2 * sizeof(RsTab) + 8);

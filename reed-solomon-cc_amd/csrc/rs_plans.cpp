@@ -32,15 +32,16 @@ void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
 
 // The reconstruct of one erasure pattern (root.zig:268-335) as an n_in -> e map.
 // Inputs: every present original + the first e present recovery shards (exactly k:
-// the unique restored data does not depend on which k). Under D1 the literal
-// reconstruct is not a decoder, so its output depends on the pattern: keep ALL
-// present shards then, exactly as the reference would receive them.
+// the unique restored data does not depend on which k). Under D1, and under D2 where
+// it drops a chunk, the literal reconstruct is no decoder of the parity, so its output
+// depends on every present shard: keep ALL of them then, exactly as the reference would
+// receive them (literal_decode).
 void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns) {
   const bool d1 = flags & RS_FLAG_QUIRK_D1;
   const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
   uint64_t present_count = 0;
   for (uint64_t i = 0; i < k + m; i++) present_count += present[i] ? 1 : 0;
-  const uint64_t want = d1 ? present_count : k;
+  const uint64_t want = literal_decode(k, m, flags) ? present_count : k;
   std::vector<uint8_t> received(W, 0);
   std::vector<uint64_t> in_pos, out_pos;
   ns.role = "reconstruct";
@@ -262,7 +263,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   int kind = decode_kind(k, m, flags, e, present_count, sb);
   // bit-sliced network (rs_jit.hpp): the same e x k map as the matrix kernels at a
   // fraction of their VALU cost, so preferred whenever it applies (modes auto / net)
-  const uint64_t n_in_want = d1 ? present_count : k;
+  const uint64_t n_in_want = literal_decode(k, m, flags) ? present_count : k;
   const bool use_net = (mode == "auto" || mode == "net") && jit::enabled() &&
                        jit::supports(static_cast<uint32_t>(n_in_want), static_cast<uint32_t>(e), sb);
   if (use_net && kind == 0) kind = e <= kMatrixMaxOut ? 1 : 2;  // table kernels stay as the fallback
@@ -283,9 +284,11 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     out = lite;
     if (!lite->upgrading.exchange(true)) {
       std::vector<uint8_t> pres(present, present + k + m);
+      // the job also queues the full plan's network compile (behind it on the worker, so
+      // rs_net_wait returns only once the pattern's steady-state kernel is loaded)
       if (!jit::run_host_job("plan:" + key, [dev, k, m, sb, flags, pres] {
             std::shared_ptr<DecodePlan> p;
-            (void)get_decode_plan(dev, k, m, sb, flags, pres.data(), p, 2);
+            if (get_decode_plan(dev, k, m, sb, flags, pres.data(), p, 2) == RS_OK && p && p->net) queue_net(*p->net, sb);
           }))
         lite->upgrading = false;
     }

@@ -362,6 +362,7 @@ hipError_t launch_solve(const jit::Kernel &kn, const uint8_t *rec, uint64_t rs_,
   if (cs == 0 || cs % kSolveMaxOut || cs > 64 || plan_dw < hdr + 2 + 64 + 64 * cs) return hipErrorInvalidValue;
   const uint32_t groups = cs / kSolveMaxOut;
   const uint64_t gx = (sb / jit::kUnitBytes + 3) / 4;
+  trace_launch(kn.name.c_str());
   for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
     const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
     const unsigned char *a0 = rec, *a1 = scratch;
@@ -403,6 +404,7 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *orig, uin
   if (!supports(s.k, s.m, sb)) return hipErrorInvalidValue;
   const uint64_t units = sb / jit::kUnitBytes, gx = (units + 3) / 4;
   if (gx > 0x7fffffffull) return hipErrorInvalidValue;
+  trace_launch(kn.name.c_str());
   for (uint64_t s0 = 0; s0 < n_stripes; s0 += 65535) {
     const uint32_t gy = static_cast<uint32_t>(std::min<uint64_t>(65535, n_stripes - s0));
     const unsigned char *a0 = orig, *a1 = rec;

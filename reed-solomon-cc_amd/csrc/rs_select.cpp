@@ -119,7 +119,7 @@ bool direct_net_async(uint64_t e, uint64_t n_in, uint64_t sb, const std::string 
 // against 0.75*200*55). Needs the corrected multiply (under D1 the literal
 // reconstruct is no inverse of the encode) and a fused (non-generic) encode kernel.
 bool syndrome_pick(uint64_t k, uint64_t m, uint64_t e, uint32_t flags, uint64_t sb, const std::string &mode) {
-  if ((flags & RS_FLAG_QUIRK_D1) || e == 0 || e > kMtileMaxOut || sb % 512) return false;
+  if (literal_decode(k, m, flags) || e == 0 || e > kMtileMaxOut || sb % 512) return false;
   if (choose_encode(k, m, sb, 4).variant == Variant::kGeneric) return false;
   if (mode == "syndrome") return true;
   if (mode != "auto") return false;

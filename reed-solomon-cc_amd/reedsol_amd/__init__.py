@@ -88,6 +88,8 @@ def lib():
         "rs_reconstruct_kernel_name": (C.c_char_p, [u64, u64, sz, vp]),
         "rs_net_compile_check": (C.c_int, [u64, u64, vp, u32, vp]),
         "rs_net_wait": (C.c_int, []),
+        "rs_reconstruct_warm": (C.c_int, [u64, u64, sz, vp, u32]),
+        "rs_last_kernels": (C.c_char_p, []),
         "rs_jit_stats": (C.c_int, [vp, vp, vp]),
         "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
         "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
@@ -406,8 +408,23 @@ def fft_decode_selftest(k, m, erased, trials=8) -> int:
 
 
 def net_wait() -> None:
-    """Block until no background network compile is running (include/reedsol.h)."""
+    """Block until no background plan build or network compile is queued or running
+    (include/reedsol.h)."""
     _check(lib().rs_net_wait())
+
+
+def reconstruct_warm(k, m, shard_bytes, present, flags: int = FLAG_CORRECTED) -> None:
+    """Drive one erasure pattern to its steady state (full plan, every kernel its calls
+    launch compiled and loaded), blocking; include/reedsol.h rs_reconstruct_warm."""
+    pres = (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
+    _check(lib().rs_reconstruct_warm(k, m, shard_bytes, pres, flags))
+
+
+def last_kernels() -> list:
+    """Kernels the calling thread's most recent compute call launched, in order
+    (hipRTC kernels by their symbol, as rocprofv3 names them)."""
+    t = lib().rs_last_kernels().decode()
+    return t.split(";") if t else []
 
 
 # ------------------------------------------------------------ engine test shims

@@ -109,6 +109,11 @@ def test_device_entry_points_fail_loudly_without_gpu():
         R.encode(4, 2, [bytes(64)] * 4)
     with pytest.raises(R.NoDevice):
         R.engine_mul_scalar(bytearray(64), 7)
+    with pytest.raises(R.NoDevice):
+        R.reconstruct_warm(10, 4, 4096, [0] + [1] * 13)
+    assert R.last_kernels() == []  # nothing launched by the failed call
+    with pytest.raises(R.NotEnoughShards):  # validation first
+        R.reconstruct_warm(10, 4, 4096, [0] * 5 + [1] * 9)
 
 
 def test_kernel_selection_network(monkeypatch):

@@ -537,7 +537,7 @@ def test_per_stripe_mid_band(oracle, monkeypatch, k, m, sb, n, flags, max_e):
     c = 1 << (m - 1).bit_length()
     if flags & 2 and k > c and k % c == 0:  # D2 drops the last chunk: not MDS, the reference decode as written
         assert path == "pattern_fft"
-        pytest.skip("D2-dropping code: covered against the oracle by test_reconstruct_per_stripe_patterns")
+        pytest.skip("D2-dropping code: covered against the oracle by test_per_stripe_patterns_d2_dropping")
     assert path in (f"psyn_k{k}_m{m}", "fft_decode", "fft_syndromes+psyn_solve"), path
     rng = np.random.default_rng(k * 11 + m + flags + max_e)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
@@ -561,6 +561,59 @@ def test_per_stripe_mid_band(oracle, monkeypatch, k, m, sb, n, flags, max_e):
         got = missing[:max_e]
         assert (out[s, :len(got)] == data[s, got]).all(), (s, missing)
         assert (out[s, len(got):] == 0xAB).all(), s
+
+
+@pytest.mark.parametrize("k,m,sb", [(8, 4, 4096), (100, 4, 4096), (32, 8, 8192), (4, 2, 2048), (64, 16, 4096),
+                                    (128, 32, 2048)])
+@pytest.mark.parametrize("flags", [2, 3])
+def test_per_stripe_patterns_d2_dropping(oracle, k, m, sb, flags):
+    """Codes whose D2 schedule drops the last full chunk (root.zig:151: k > chunk, k % chunk
+    == 0): the parity ignores those shards, so the literal reconstruct (root.zig:268-335)
+    is no decoder and its output depends on every present shard. Per-stripe patterns on
+    such codes must reproduce it exactly: against oracle.reconstruct_batch(quirks=flags)
+    stripe by stripe, with surplus recovery shards present in most stripes."""
+    n = 7
+    rng = np.random.default_rng(k * 17 + m + flags)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=flags, threads=8)
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n):
+        e = int(rng.integers(1, m + 1)) if s else m  # stripe 0: exactly k present
+        present[s, rng.choice(k, size=e, replace=False)] = 0
+        extra = m - e if s == 0 else int(rng.integers(0, m - e + 1))
+        present[s, k + rng.choice(m, size=extra, replace=False)] = 0
+    max_e = m
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=DEV)
+    status = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    R.reconstruct_batch_dev_patterns(k, m, to_dev(present), to_dev(data), to_dev(par), out, status, flags)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    for s in range(n):
+        assert status[s] == 0, s
+        missing = [i for i in range(k) if not present[s, i]]
+        exp = oracle.reconstruct_batch(k, m, present[s], np.concatenate([data[s:s + 1], par[s:s + 1]], axis=1),
+                                       quirks=flags)
+        assert (out[s, :len(missing)] == exp[0]).all(), (s, missing)
+        assert (out[s, len(missing):] == 0xAB).all(), s
+
+
+@pytest.mark.parametrize("k,m", [(8, 4), (100, 4), (32, 8), (128, 32)])
+def test_batch_reconstruct_d2_dropping(oracle, k, m):
+    """The same for one pattern per batch under D2 alone (flags 2: the corrected multiply,
+    so every path but the literal map would otherwise be eligible), surplus shards present."""
+    sb, n = 4096, 3
+    rng = np.random.default_rng(k * 5 + m)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, quirks=2)
+    shards = np.concatenate([data, par], axis=1)
+    for trial in range(3):
+        e = int(rng.integers(1, m + 1))
+        present = np.ones(k + m, np.uint8)
+        present[rng.choice(k, size=e, replace=False)] = 0
+        present[k + rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)] = 0
+        got = gpu_reconstruct(k, m, present, data, par, 2)
+        exp = oracle.reconstruct_batch(k, m, present, shards, quirks=2)
+        assert (got == exp).all(), (k, m, trial, R.reconstruct_kernel_name(k, m, sb, present))
 
 
 @pytest.mark.parametrize("sb", [2, 6, 66, 70, 1000, 4102])

@@ -1,0 +1,108 @@
+"""Which kernel a reconstruct actually launches (rs_last_kernels) and the warm-up recipes of
+include/reedsol.h / INTEGRATION.md: a wide-code pattern's first calls run the fused FFT
+reconstruct (the pattern as data); where the pattern's e x e syndrome network beats it, two
+calls + rs_net_wait, or one rs_reconstruct_warm, bring the pattern to that network, and the
+next call launches it. Restored shards are checked against the data every time (MDS:
+restored originals are unique). Reference: root.zig:268-335 (Decoder.decode)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+from rs_amd import reedsol_amd as R  # noqa: E402
+
+DEV = torch.device("cuda:0")
+K, M, SB, N = 200, 55, 4096, 4
+
+
+@pytest.fixture(scope="module")
+def c4_batch(oracle):
+    rng = np.random.default_rng(0xC4C4)
+    data = rng.integers(0, 256, (N, K, SB), dtype=np.uint8)
+    par = oracle.encode_batch(K, M, data, threads=4)
+    return torch.from_numpy(data).to(DEV), torch.from_numpy(par).to(DEV)
+
+
+def pattern(seed, e=M):
+    lost = sorted(int(i) for i in np.random.default_rng(seed).choice(K, size=e, replace=False))
+    present = [0 if i in lost else 1 for i in range(K)] + [1] * M
+    return lost, present
+
+
+def run(present, lost, batch):
+    d, p = batch
+    out = torch.zeros((N, len(lost), SB), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(K, M, present, d, p, out)
+    ran = R.last_kernels()
+    torch.cuda.synchronize()
+    assert torch.equal(out, d[:, lost])
+    return ran
+
+
+def has(ran, prefix):
+    return any(k.startswith(prefix) for k in ran)
+
+
+def test_last_kernels_headline_shapes():
+    """RS(10,4) encode and reconstruct report the networks rocprofv3 shows (bench labels)."""
+    k, m, sb, n = 10, 4, 4096, 8
+    d = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8, device=DEV)
+    p = torch.empty((n, m, sb), dtype=torch.uint8, device=DEV)
+    R.encode_batch_dev(k, m, d, p)
+    assert R.last_kernels() and R.last_kernels()[0].startswith("rs_net_encode_i10_o4")
+    present = [0, 0, 0, 0] + [1] * (k + m - 4)
+    out = torch.empty((n, 4, sb), dtype=torch.uint8, device=DEV)
+    R.reconstruct_batch_dev(k, m, present, d, p, out)
+    assert R.last_kernels()[0].startswith("rs_net_reconstruct_i10_o4")
+    torch.cuda.synchronize()
+    assert torch.equal(out, d[:, :4])
+
+
+def test_first_call_runs_fused(c4_batch, monkeypatch):
+    monkeypatch.delenv("RS_AMD_FDEC", raising=False)
+    lost, present = pattern(401)
+    ran = run(present, lost, c4_batch)
+    assert has(ran, "rs_fft_decode_k200_m55"), ran
+
+
+def test_warm_reaches_network(c4_batch, monkeypatch):
+    """rs_reconstruct_warm: the next call launches the pattern's 55 x 55 syndrome network."""
+    monkeypatch.delenv("RS_AMD_FDEC", raising=False)
+    lost, present = pattern(402)
+    R.reconstruct_warm(K, M, SB, present)
+    ran = run(present, lost, c4_batch)
+    assert has(ran, "rs_net_syndrome_i55_o55"), ran
+    assert not has(ran, "rs_fft_decode"), ran
+
+
+def test_two_calls_and_net_wait_reach_network(c4_batch, monkeypatch):
+    """The INTEGRATION.md recipe without the warm call: two calls, rs_net_wait, then the
+    network (the upgrade job queues the compile behind the plan build)."""
+    monkeypatch.delenv("RS_AMD_FDEC", raising=False)
+    lost, present = pattern(403)
+    assert has(run(present, lost, c4_batch), "rs_fft_decode")
+    run(present, lost, c4_batch)
+    R.net_wait()
+    ran = run(present, lost, c4_batch)
+    assert has(ran, "rs_net_syndrome_i55_o55"), ran
+
+
+def test_forced_fused_after_warm(c4_batch, monkeypatch):
+    monkeypatch.setenv("RS_AMD_FDEC", "1")
+    lost, present = pattern(404)
+    R.reconstruct_warm(K, M, SB, present)
+    ran = run(present, lost, c4_batch)
+    assert has(ran, "rs_fft_decode_k200_m55") and not has(ran, "rs_net_syndrome"), ran
+
+
+def test_few_losses_stay_fused_or_direct(c4_batch, monkeypatch):
+    """20 losses: the fused kernel is the steady state (no network beats it)."""
+    monkeypatch.delenv("RS_AMD_FDEC", raising=False)
+    lost, present = pattern(405, e=20)
+    R.reconstruct_warm(K, M, SB, present)
+    ran = run(present, lost, c4_batch)
+    assert has(ran, "rs_fft_decode_k200_m55"), ran
