@@ -219,6 +219,20 @@ int rs_reconstruct_warm(uint64_t original_count, uint64_t recovery_count, size_t
  * worker threads and are recorded there, not here. Valid until the thread's next call. */
 const char *rs_last_kernels(void);
 
+/* ------------------------------------------------ fault injection (tests only)
+ * The reference runs its encode under std.testing.checkAllAllocationFailures
+ * (tests.zig:131-156): every allocation of the call fails in turn and must surface as
+ * error.OutOfMemory with nothing leaked. Here every allocation the library makes — plan
+ * objects, device and stream-ordered buffers, pinned staging — is counted; after
+ * rs_debug_fail_alloc(n) the n-th one (from 0, all threads) fails as if out of memory and
+ * the call returns RS_ERR_OUT_OF_MEMORY. n < 0 disarms. Returns the number of allocations
+ * counted since the previous rs_debug_fail_alloc call. */
+int64_t rs_debug_fail_alloc(int64_t n);
+/* Drop every cache holding device or pinned memory (plans, device tables, staging rings,
+ * pooled one-shot contexts; compiled kernels stay loaded), after any background plan build
+ * finished. *pooled_contexts (optional) = one-shot contexts left in the pool (0). */
+int rs_debug_release_caches(uint64_t *pooled_contexts);
+
 /* hipRTC activity of this process: kernels compiled, code objects found in the on-disk
  * cache ($RS_AMD_CACHE_DIR, else $XDG_CACHE_HOME/rs_amd or ~/.cache/rs_amd; empty = off),
  * modules loaded. Any pointer may be NULL. */
@@ -262,6 +276,11 @@ int rs_fft_selftest(uint64_t original_count, uint64_t recovery_count, uint32_t f
  * kernel or e > recovery_count. */
 int rs_fft_decode_compile_check(uint64_t original_count, uint64_t recovery_count, double *compile_ms,
                                 uint64_t *code_bytes);
+/* The same kernel with one erasure pattern compiled in (present: k + m flags): the locator
+ * scalars as constant multiplies, rows, blocks and outputs static (the steady state of a
+ * pattern reused across batches). RS_ERR_NOT_ENOUGH_SHARDS if the pattern cannot decode. */
+int rs_fft_pdecode_compile_check(uint64_t original_count, uint64_t recovery_count, const uint8_t *present,
+                                 double *compile_ms, uint64_t *code_bytes);
 int rs_fft_decode_selftest(uint64_t original_count, uint64_t recovery_count, uint32_t erased, int trials,
                            uint64_t *mismatches);
 

@@ -37,7 +37,7 @@ int encode_tail(uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint8_t *
   const uint64_t psb = (sb + 63) / 64 * 64;
   const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n, kTailSliceBytes / ((k + m) * psb)));
   void *buf = nullptr;
-  HIP_TRY(hipMallocAsync(&buf, cap * (k + m) * psb, s));
+  HIP_TRY(dev_malloc_async(&buf, cap * (k + m) * psb, s));
   uint8_t *pin = static_cast<uint8_t *>(buf), *pout = pin + cap * k * psb;
   int st = RS_OK;
   for (uint64_t s0 = 0; st == RS_OK && s0 < n; s0 += cap) {
@@ -58,7 +58,7 @@ int reconstruct_tail(uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const uint
   const uint64_t psb = (sb + 63) / 64 * 64;
   const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n, kTailSliceBytes / ((k + m + e) * psb)));
   void *buf = nullptr;
-  HIP_TRY(hipMallocAsync(&buf, cap * (k + m + e) * psb, s));
+  HIP_TRY(dev_malloc_async(&buf, cap * (k + m + e) * psb, s));
   uint8_t *po = static_cast<uint8_t *>(buf), *pr = po + cap * k * psb, *pout = pr + cap * m * psb;
   int st = RS_OK;
   for (uint64_t s0 = 0; st == RS_OK && s0 < n; s0 += cap) {
@@ -156,7 +156,7 @@ int rs_encode_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_stripes, c
     }
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
     void *scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
+    HIP_TRY(dev_malloc_async(&scratch, per * plan->work * sb, s));
     for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
       EncodeArgs b = a;
       b.data += s0 * orig_stride;
@@ -230,6 +230,16 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     // for the pattern is loaded (as fast for the syndrome maps, faster for few losses)
     if (plan->fdec_blk && max_nv == 4 && fdec_supports(k, m, sb, flags)) {
       const jit::Kernel *nk = plan->net && fdec_mode() != 1 ? net_kernel(*plan->net, sb) : nullptr;
+      if (!nk && plan->pdec && pdec_enabled()) {  // the pattern compiled in, once loaded
+        const fftnet::Spec *pfs = nullptr;
+        if (const jit::Kernel *pk = fft_kernel(*plan->pdec, sb, &pfs)) {
+          HIP_TRY(fftnet::launch(*pk, *pfs, static_cast<const uint8_t *>(d_original ? d_original : d_recovery),
+                                 orig_stride, static_cast<const uint8_t *>(d_recovery), rec_stride,
+                                 static_cast<uint8_t *>(d_restored), out_stride, sb, n_stripes,
+                                 static_cast<hipStream_t>(stream)));
+          return RS_OK;
+        }
+      }
       if (!nk) {
         std::shared_ptr<WpsSlot> ws;
         wps_slot(dev, k, m, 0, ws);
@@ -321,7 +331,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       const uint64_t cap = 4096ull << 20;
       const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, cap / (m * sb)));
       void *scratch = nullptr;
-      HIP_TRY(hipMallocAsync(&scratch, per * m * sb, s));
+      HIP_TRY(dev_malloc_async(&scratch, per * m * sb, s));
       for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
         const uint64_t cnt = std::min(per, n_stripes - s0);
         EncodeArgs eb = ea;
@@ -367,7 +377,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     }
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
     void *scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
+    HIP_TRY(dev_malloc_async(&scratch, per * plan->work * sb, s));
     for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
       DecodeArgs b = a;
       b.orig += s0 * orig_stride;
@@ -419,6 +429,8 @@ int rs_reconstruct_warm(uint64_t k, uint64_t m, size_t sb, const uint8_t *presen
     const fftnet::Spec *fs = nullptr;
     if (plan->inv_fft) (void)fft_kernel(*plan->inv_fft, psb, &fs);
     if (plan->net) queue_net(*plan->net, psb);
+    // a build that spills is rebuilt with less prefetch (fftnet::get): a few rounds
+    for (int i = 0; i < 4 && plan->pdec && !fft_kernel(*plan->pdec, psb, &fs); i++) jit::wait_pending();
     if (plan->fdec_blk && fdec_supports(k, m, psb, flags)) {
       std::shared_ptr<WpsSlot> ws;
       wps_slot(dev, k, m, 0, ws);

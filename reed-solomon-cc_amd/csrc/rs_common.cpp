@@ -16,7 +16,53 @@ int hip_fail(hipError_t e, const char *what) {
   // the failed call also set the thread's last HIP error: reset it, so the caller's next
   // hipGetLastError (e.g. torch's launch check) does not report this call's failure
   (void)hipGetLastError();
-  return fail(RS_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+  return fail(e == hipErrorOutOfMemory ? RS_ERR_OUT_OF_MEMORY : RS_ERR_DEVICE,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// ------------------------------------------------------ allocation-failure injection
+namespace {
+std::atomic<int64_t> g_fail_at{-1};  // index of the allocation that fails (-1: off)
+std::atomic<int64_t> g_allocs{0};    // allocations counted since rs_debug_fail_alloc
+}  // namespace
+
+bool alloc_fails() {
+  const int64_t i = g_allocs.fetch_add(1);
+  return i == g_fail_at.load();
+}
+
+void alloc_point() {
+  if (alloc_fails()) throw std::bad_alloc();
+}
+
+hipError_t dev_malloc(void **p, size_t bytes) {
+  if (alloc_fails()) {
+    *p = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  return hipMalloc(p, bytes);
+}
+
+hipError_t dev_malloc_async(void **p, size_t bytes, hipStream_t s) {
+  if (alloc_fails()) {
+    *p = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  return hipMallocAsync(p, bytes, s);
+}
+
+hipError_t pinned_malloc(void **p, size_t bytes) {
+  if (alloc_fails()) {
+    *p = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  return hipHostMalloc(p, bytes, hipHostMallocDefault);
+}
+
+int64_t arm_alloc_failure(int64_t n) {
+  const int64_t seen = g_allocs.exchange(0);
+  g_fail_at.store(n < 0 ? -1 : n);
+  return seen;
 }
 
 
@@ -220,7 +266,7 @@ int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out
   thread_local std::map<int, hipStream_t> streams;
   auto b = std::make_shared<DevBuf>();
   b->dev = dev;
-  HIP_TRY(hipMalloc(&b->p, std::max<size_t>(bytes, 16)));
+  HIP_TRY(dev_malloc(&b->p, std::max<size_t>(bytes, 16)));
   hipStream_t &st = streams[dev];
   if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   HIP_TRY(hipMemcpyAsync(b->p, host, bytes, hipMemcpyHostToDevice, st));
@@ -275,6 +321,25 @@ const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
 int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules) {
   return guarded([&]() -> int {
     jit::compile_stats(compiles, cache_hits, modules);
+    return RS_OK;
+  });
+}
+
+int64_t rs_debug_fail_alloc(int64_t n) { return arm_alloc_failure(n); }
+
+int rs_debug_release_caches(uint64_t *pooled_contexts) {
+  return guarded([&]() -> int {
+    jit::wait_pending();  // no plan build on the worker holds a plan being dropped
+    release_plans();
+    release_patterns();
+    release_lowrate();
+    release_oneshot();
+    release_host_rings();
+    {
+      std::lock_guard<std::mutex> lk(g_plan_mu);
+      g_twiddle_plans.clear();
+    }
+    if (pooled_contexts) *pooled_contexts = oneshot_pooled();
     return RS_OK;
   });
 }

@@ -94,6 +94,8 @@ struct Layer {
 
 uint16_t sk(uint64_t idx) { return idx < kModulus ? tables().skew[idx] : static_cast<uint16_t>(kModulus); }
 
+uint16_t gmul_elem(uint16_t x, uint16_t y) { return x && y ? mul16(x, tables().log[y]) : 0; }
+
 int log2i(uint64_t v) {
   int b = 0;
   while ((1ull << b) < v) b++;
@@ -200,13 +202,22 @@ Plan make_plan(const Spec &s) {
     std::vector<uint8_t> v(p.C, 0);
     for (uint32_t q = 0; q < p.C; q++) {
       const uint64_t g = j * p.C + q;
-      v[q] = g < s.k && !(g < s.skip.size() && s.skip[g]);
+      v[q] = g < s.k && !(g < s.skip.size() && s.skip[g]) && !(g < s.present.size() && !s.present[g]);
     }
     p.valid.push_back(std::move(v));
   }
   p.fft = fft_layers(p.C, s.inverse ? s.k : s.m, s.inverse ? p.C : 0);  // root.zig:169
   p.out_mode.assign(p.C, kOutNone);
   for (uint32_t q = 0; q < s.m; q++) p.out_mode[q] = s.out_mode.empty() ? kOutStore : s.out_mode[q];
+  if (!s.present.empty()) {  // static decode: Enc(d') is needed on the rows R only
+    uint32_t e = 0, nr = 0;
+    for (uint32_t g = 0; g < s.k; g++) e += s.present[g] ? 0 : 1;
+    for (uint32_t q = 0; q < s.m; q++) {
+      const bool in_r = s.present[s.k + q] && nr < e;
+      nr += in_r ? 1 : 0;
+      p.out_mode[q] = in_r ? kOutStore : kOutNone;
+    }
+  }
   return p;
 }
 
@@ -282,18 +293,47 @@ __device__ __forceinline__ void unplanes2(u32 *P, v4 &a, v4 &b) {
 // (scalar_masks), read through the constant address space (scalar loads):
 // out_i = XOR_j (x_j & M[16 i + j]) ^ (SWN(x_j) & M[16 i + 8 + j])
 typedef const __attribute__((address_space(4))) u32 *cptr;
+// RS_RMUL_G output planes per step: their 16 G masks are read together (one scalar-load
+// wait per step instead of per plane) and their chains interleave
+#ifndef RS_RMUL_G
+#define RS_RMUL_G 1
+#endif
 __device__ __forceinline__ void rmul(u32 *x, cptr M) {
+#ifdef RS_DBG_NORMUL
+  return;
+#endif
   u32 s[8], o[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) s[j] = SWN(x[j]);
+#ifdef RS_RMUL_VLOAD
+  // masks through vector loads (a laundered zero VGPR offset keeps them off the scalar
+  // path): in-order vmcnt lets the compiler keep several planes' masks in flight
+  u32 vz = 0;
+  asm volatile("" : "+v"(vz));
+  const v4 *M4 = (const v4 *)(const void *)M + vz;
+#endif
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    u32 a = x[0] & M[16 * i];
+  for (int i0 = 0; i0 < 8; i0 += RS_RMUL_G) {
+    u32 m[16 * RS_RMUL_G];
+#ifdef RS_RMUL_VLOAD
 #pragma unroll
-    for (int j = 1; j < 8; j++) a = __builtin_amdgcn_bitop3_b32(a, x[j], M[16 * i + j], 0x78);
+    for (int t = 0; t < 4 * RS_RMUL_G; t++) {
+      const v4 q = M4[4 * i0 + t];
+      m[4 * t] = q[0]; m[4 * t + 1] = q[1]; m[4 * t + 2] = q[2]; m[4 * t + 3] = q[3];
+    }
+#else
 #pragma unroll
-    for (int j = 0; j < 8; j++) a = __builtin_amdgcn_bitop3_b32(a, s[j], M[16 * i + 8 + j], 0x78);
-    o[i] = a;
+    for (int t = 0; t < 16 * RS_RMUL_G; t++) m[t] = M[16 * i0 + t];
+#endif
+#pragma unroll
+    for (int g = 0; g < RS_RMUL_G; g++) {
+      u32 a = x[0] & m[16 * g];
+#pragma unroll
+      for (int j = 1; j < 8; j++) a = __builtin_amdgcn_bitop3_b32(a, x[j], m[16 * g + j], 0x78);
+#pragma unroll
+      for (int j = 0; j < 8; j++) a = __builtin_amdgcn_bitop3_b32(a, s[j], m[16 * g + 8 + j], 0x78);
+      o[i0 + g] = a;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 8; i++) x[i] = o[i];
@@ -312,10 +352,22 @@ int env_int(const char *name, int def) {
 int sched_of() { return 1; }
 
 int prefetch_of(const Spec &s) {
-  // the decode tail keeps the IFFT result live across its blocks: no register room for
-  // the next unit's loads (prefetch 2 spills, 0 does not: 241 VGPRs for RS(200,55))
-  const int def = s.decode ? 0 : 4;
-  return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", def)));
+  return std::max(0, std::min(8, s.prefetch >= 0 ? s.prefetch : env_int("RS_AMD_FFT_PREFETCH", 4)));
+}
+
+// RS_AMD_FFT_DEBUG (measurement builds only, part of the cache key): bit 0 loads read
+// through the zero-record resource (no HBM reads), bit 1 stores dropped the same way, bit 2
+// decode kernels stop after Enc(d') (no decode tail), bit 3 decode: no runtime multiplies,
+// bit 4 decode: the round-3 load order (rec rows loaded at the tail, no prefetch)
+int debug_of() { return env_int("RS_AMD_FFT_DEBUG", 0); }
+
+// runtime-multiply masks through vector loads (RS_AMD_FFT_RMULV=1) instead of scalar loads
+int rmul_vload() { return env_int("RS_AMD_FFT_RMULV", 0) ? 1 : 0; }
+
+// runtime-multiply output planes per scalar-load step (RS_AMD_FFT_RMULG: 1, 2, 4, 8)
+int rmul_group() {
+  const int g = env_int("RS_AMD_FFT_RMULG", 1);
+  return g == 2 || g == 4 || g == 8 ? g : 1;
 }
 
 struct Gen {
@@ -555,7 +607,43 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // non-temporal loads and stores (cache policy bit nt = 2): RS(200,55) 256 KiB encode
   // 3.84 -> 3.70 ms (profiles/r02/fft_sweep_*.jsonl)
   const bool dyn = s.dyn;
-  o << "#define RS_AUX_LD 2\n#define RS_AUX_ST 2\n" << kPrelude;
+  const int dbg = debug_of();
+  // decode kernels: the recovery rows R are loaded before the final FFT's B layers (in
+  // flight during them, the B -> A exchange and the A layers), the next unit's leading
+  // chunk-0 positions before the last data block (the IFFT result is dead from there);
+  // RS_AMD_FFT_DEBUG bit 4: the round-3 order (rows loaded at the tail, no prefetch)
+  const bool old_order = s.decode && (dbg & 16);
+  const bool tail = s.decode && !(dbg & 4);
+  // Spec::present: the pattern compiled in (rows R, locator constants, outputs, blocks)
+  const bool spat = s.decode && !s.present.empty();
+  std::vector<uint8_t> inR(C, 0);         // recovery row p is one of the rows R
+  std::vector<uint16_t> lp_log(C, 0);     // log of L_p (row p in R)
+  std::vector<int32_t> out_row(s.k, -1);  // output row of erased data shard g
+  std::vector<uint32_t> cg_log(s.k, 0);   // log of L'_g beta_K (kModulus + 1: zero)
+  if (spat) {
+    const Tables &T = tables();
+    uint32_t e = 0, nr = 0;
+    for (uint32_t g = 0; g < s.k; g++) e += s.present[g] ? 0 : 1;
+    std::vector<uint8_t> received(ceil_pow2(C + s.k), 0);
+    for (uint32_t p = 0; p < s.m && nr < e; p++)
+      if (s.present[s.k + p]) received[p] = inR[p] = 1, nr++;
+    for (uint32_t g = 0; g < s.k; g++) received[C + g] = s.present[g] ? 1 : 0;
+    std::vector<uint16_t> er(kOrder);
+    erasure_logs(received.data(), s.k, s.m, er.data());  // root.zig:277-289, as decode_block
+    std::vector<uint16_t> beta;
+    decode_betas(s.k, s.m, beta);
+    for (uint32_t p = 0; p < s.m; p++)
+      if (inR[p]) lp_log[p] = T.log[T.exp[er[p]]];  // root.zig:292-295
+    int32_t row = 0;
+    for (uint32_t g = 0; g < s.k; g++)
+      if (!s.present[g]) {
+        out_row[g] = row++;
+        const uint16_t c = gmul_elem(beta[(C + g) / C], T.exp[kModulus - er[C + g]]);  // root.zig:321-326
+        cg_log[g] = c ? T.log[c] : kModulus + 1u;
+      }
+  }
+  o << "#define RS_AUX_LD 2\n#define RS_AUX_ST 2\n" << (s.decode && (dbg & 8) ? "#define RS_DBG_NORMUL 1\n" : "")
+    << "#define RS_RMUL_G " << rmul_group() << "\n" << (rmul_vload() ? "#define RS_RMUL_VLOAD 1\n" : "") << kPrelude;
   // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
   // batch, so its loads read zeros and its stores are dropped)
@@ -567,6 +655,11 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   // name = rsrc(stripe0) [, name1 = rsrc(stripe0 + 1) or RZ]; `guard`: the unit exists
   auto rsrc_pair = [&](std::ostream &os_, const char *name, const char *base, const char *stride, const std::string &st0,
                        uint32_t rows, const std::string &guard) {
+    const std::string nm = name;
+    if (((dbg & 1) && (nm == "RD" || nm == "RR" || nm == "RDn")) || ((dbg & 2) && nm == "RO")) {  // measurement builds
+      os_ << "  const __amdgpu_buffer_rsrc_t " << name << " = RZ, " << name << "1 = RZ;\n";
+      return;
+    }
     const std::string s0 = two ? "(" + st0 + ") * 2u" : st0;
     os_ << "  const __amdgpu_buffer_rsrc_t " << name << " = " << (guard.empty() ? "" : guard + " ? ")
         << rsrc(base, stride, s0, rows) << (guard.empty() ? "" : " : RZ") << ";\n";
@@ -618,7 +711,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   rsrc_pair(hdr2, "RD", "data", "ds", "stripe", s.k, "");
   rsrc_pair(hdr2, "RO", "out", "os", "stripe", s.m, "");
   if (dyn) hdr2 << "  const u32 *DM = dm + stripe * dmw;\n";
-  if (s.decode) hdr2 << "  const cptr DMc = (cptr)DM;\n";
+  if (s.decode && dyn) hdr2 << "  const cptr DMc = (cptr)DM;\n";
   if (any_xor) rsrc_pair(hdr2, "RR", "rec", "rs", "stripe", s.m, "");
   hdr2 << "  u32 ";
   for (uint32_t r = 0; r < 8; r++)
@@ -676,12 +769,14 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   std::vector<uint8_t> acc_live(8, 0);  // layout B regs of the accumulator
   // RS_AMD_FFT_PREFETCH: positions of the next chunk loaded before this chunk's layers
   // (the rest just before their plane transform)
-  const uint32_t pf = static_cast<uint32_t>(prefetch_of(s));
-  // the next unit's first pf positions are loaded during this unit's FFT
+  const uint32_t pf = old_order ? 0u : static_cast<uint32_t>(prefetch_of(s));
+  // the next unit's first pfu positions are loaded during this unit's FFT (encode) or
+  // before its last data block (decode)
+  const uint32_t pfu = pf;
   declared[0] = 1;  // la0 / lb0 live across units (cross-unit prefetch)
-  std::vector<uint32_t> vm_next = emit_loads(0, 0, pf);
+  std::vector<uint32_t> vm_next = emit_loads(0, 0, pfu);
   o << "  }\n" << hdr2.str();
-  emit_loads(0, pf, 8);
+  emit_loads(0, pfu, 8);
   for (size_t j = 0; j < P.truncs.size(); j++) {
     const std::vector<uint32_t> vm = vm_next;
     if (j > 0) emit_loads(j, pf, 8);
@@ -788,6 +883,37 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     }
     need = nd;
   }
+  // decode: the recovery rows R of this wave's 8 positions (layout A), in flight during the
+  // FFT's B layers, its exchange and its A layers
+  const uint32_t dwm = dyn_store_word(P) + 2;
+  auto emit_rec_loads = [&]() {
+    o << "  const u32 ub0 = DMc[" << dwm + 1 << "], ub1 = DMc[" << dwm + 2 << "];\n";
+    for (uint32_t r = 0; r < 8; r++)
+      o << "  const u32 pd" << r << " = w * 8u + " << r << "u;\n  const bool us" << r << " = ((pd" << r
+        << " < 32u ? ub0 >> pd" << r << " : ub1 >> (pd" << r << " - 32u)) & 1u) != 0u;\n  const v4 ra" << r
+        << " = LDB(us" << r << " ? RR : RZ, uo, pd" << r << " * sbl), rb" << r << " = LDB(us" << r
+        << " ? RR1 : RZ, uo1, pd" << r << " * sbl);\n";
+  };
+  if (tail && spat && (dbg & 32)) {  // static, early rows of R (measured: spills; bit 5 of RS_AMD_FFT_DEBUG)
+    o << "  v4 ";
+    for (uint32_t r = 0; r < 8; r++) o << "ra" << r << ", rb" << r << (r < 7 ? ", " : ";\n");
+    bool firstw = true;
+    for (uint32_t w = 0; w < NW; w++) {
+      bool any = false;
+      for (uint32_t r = 0; r < 8; r++) any |= P.posA(w, r) < s.m && inR[P.posA(w, r)];
+      if (!any) continue;
+      o << "  " << (firstw ? "if" : "else if") << " (w == " << w << "u) {\n";
+      firstw = false;
+      for (uint32_t r = 0; r < 8; r++) {
+        const uint32_t p = P.posA(w, r);
+        if (p < s.m && inR[p])
+          o << "  ra" << r << " = LDB(RR, uo, " << p << "u * sbl); rb" << r << " = LDB(RR1, uo1, " << p << "u * sbl);\n";
+      }
+      o << "  }\n";
+    }
+  } else if (tail && !old_order && !spat) {
+    emit_rec_loads();
+  }
   o << "  // ---- FFT(size " << C << ", trunc " << s.m << ", skew_delta 0), Generic.zig:15-78\n";
   g.ops = &g.st->ops_b;
   bool zc[8];
@@ -802,13 +928,14 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   }
   // the next unit's leading chunk-0 positions, in flight during this unit's last exchange and stores
   o << "  u64 stripe_n = stripe + gdiv;\n  u32 uu_n = uu + gmod;\n  if (uu_n >= ups) { uu_n -= ups; stripe_n++; }\n";
-  if (pf) {
+  auto emit_next_unit_loads = [&]() {
     o << "  {\n  const u32 uon = uu_n * 2048u + loff, uon1 = " << (two ? "loff" : "uon + 1024u") << ";\n";
     rsrc_pair(o, "RDn", "data", "ds", "stripe_n", s.k, "u + step < ue");
     if (dyn) o << "  const u32 *DMn = dm + ((u + step < ue) ? stripe_n : 0ull) * dmw;\n";
-    emit_loads(0, 0, pf, "RDn", "uon", "uon1");
+    emit_loads(0, 0, pfu, "RDn", "uon", "uon1");
     o << "  }\n";
-  }
+  };
+  if (pfu && !s.decode) emit_next_unit_loads();
   // B -> A: B wave w writes reg t (position p = t << WB | w) to slot p; then every
   // wave reads its 8 slots (shared code) and passes a barrier before the
   // specialised A layers, so the next unit's first exchange may write at once
@@ -883,19 +1010,225 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     g.ops = &g.st->ops_a;
     o << "  }\n";
   }
-  if (s.decode) {
+  if (s.decode && !tail) {  // measurement build: Enc(d') only, kept live
+    for (uint32_t r = 0; r < 8; r++) {
+      o << "  asm volatile(\"\" ::";
+      for (int i = 0; i < 8; i++) o << (i ? ", " : " ") << "\"v\"(" << wname(r) << "_" << i << ")";
+      o << ");\n";
+    }
+    if (pfu) emit_next_unit_loads();
+  }
+  if (tail && spat) {
+    // ---- decode tail, pattern compiled in (Spec::present): as below, with the locator
+    // scalars as constant multiplies and every row, block and output static
+    auto cmul = [&](const std::vector<std::string> &X, uint32_t lg) {  // X *= exp[lg] in place
+      std::vector<std::string> Y(8);
+      o << "  __builtin_amdgcn_sched_barrier(0);\n  {\n  u32 ";
+      for (int i = 0; i < 8; i++) {
+        Y[i] = g.fresh("zy");
+        o << Y[i] << (i < 7 ? ", " : ";\n");
+      }
+      g.mul(Y, false, X, twiddle(static_cast<uint16_t>(lg), false));
+      for (int i = 0; i < 8; i++) o << "  " << X[i] << " = " << Y[i] << ";\n";
+      o << "  }\n";
+    };
+    const std::vector<Layer> il = ifft_layers(C, s.m, 0);
+    std::vector<uint8_t> liveB(8, 0);
+    std::vector<std::vector<uint8_t>> z0(NW, std::vector<uint8_t>(8, 1));  // zero at the IFFT's start
+    for (uint32_t w = 0; w < NW; w++) {
+      bool z[8];
+      for (uint32_t r = 0; r < 8; r++) z[r] = z0[w][r] = !(P.posA(w, r) < s.m && inR[P.posA(w, r)]);
+      for (const Layer &L : il) {
+        if (!P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf)
+          if (P.waveA(b.x) == w && !(z[P.regA(b.x)] && z[P.regA(b.y)])) z[P.regA(b.x)] = z[P.regA(b.y)] = false;
+      }
+      for (uint32_t r = 0; r < 8; r++)
+        if (!z[r]) liveB[P.regB(P.posA(w, r))] = 1;
+    }
+    // syndromes times L_p, IFFT A layers (per wave), A -> B
+    o << "  {\n  LQ();\n";
+    for (uint32_t w = 0; w < NW; w++) {
+      o << "  " << (w ? "else if" : "if") << " (w == " << w << "u) {\n";
+      if (!(dbg & 32))  // this wave's rows of R, in flight together
+        for (uint32_t r = 0; r < 8; r++)
+          if (!z0[w][r])
+            o << "  const v4 ra" << r << " = LDB(RR, uo, " << P.posA(w, r) << "u * sbl), rb" << r << " = LDB(RR1, uo1, "
+              << P.posA(w, r) << "u * sbl);\n";
+      bool z[8];
+      for (uint32_t r = 0; r < 8; r++) {
+        z[r] = z0[w][r];
+        if (z[r]) continue;
+        const uint32_t p = P.posA(w, r);
+        const auto W = Gen::regs(wname(r));
+        g.ops = &g.st->ops_io;
+        o << "  __builtin_amdgcn_sched_barrier(0);\n  { u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q);\n";
+        std::vector<std::string> q(8);
+        for (int i = 0; i < 8; i++) q[i] = "Q[" + std::to_string(i) + "]";
+        g.basis_change(q);
+        for (int i = 0; i < 8; i++) o << "  " << W[i] << " ^= Q[" << i << "];\n";
+        o << "  }\n";
+        cmul(W, lp_log[p]);
+      }
+      g.ops = &g.st->ops_a;
+      for (const Layer &L : il) {
+        if (!P.inA(L.bit)) continue;
+        for (const Bf &b : L.bf) {
+          if (P.waveA(b.x) != w) continue;
+          const uint32_t rx = P.regA(b.x), ry = P.regA(b.y);
+          g.butterfly(wname(rx), z[rx], wname(ry), z[ry], true, P.get_tw(b.log_m));
+        }
+      }
+      for (uint32_t r = 0; r < 8; r++) {
+        const uint32_t p = P.posA(w, r), t = P.regB(p);
+        if (!liveB[t]) continue;
+        std::vector<std::string> v = Gen::regs(wname(r));
+        if (z[r]) v.assign(8, "0u");
+        lds_write("0", P.waveB(p) * 8 + t, v);
+      }
+      o << "  }\n";
+    }
+    o << "  BAR();\n";
+    bool za[8];
+    for (uint32_t t = 0; t < 8; t++) {
+      za[t] = !liveB[t];
+      if (liveB[t]) lds_read("(w * 8u)", t, Gen::regs(cname(t)));
+    }
+    o << "  BAR();\n  }\n";
+    g.ops = &g.st->ops_b;
+    for (const Layer &L : il) {
+      if (P.inA(L.bit)) continue;
+      for (const Bf &b : L.bf) {
+        if (P.waveB(b.x) != 0) continue;
+        const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+        g.butterfly(cname(tx), za[tx], cname(ty), za[ty], true, P.get_tw(b.log_m));
+      }
+    }
+    for (uint32_t t = 0; t < 8; t++)
+      if (!za[t]) g.pin(Gen::regs(cname(t)));
+    // per data block K with an erasure: FFT(size C, trunc t_K, skew KC) of a, pruned to
+    // the butterflies an erased shard's evaluation needs
+    const uint32_t nblk = (s.k + C - 1) / C;
+    uint32_t last_blk = 0;
+    for (uint32_t K = 1; K <= nblk; K++)
+      for (uint32_t g0 = (K - 1) * C; g0 < std::min<uint32_t>(s.k, K * C); g0++)
+        if (!s.present[g0]) last_blk = K;
+    if (!last_blk && pfu) emit_next_unit_loads();
+    for (uint32_t K = 1; K <= last_blk; K++) {
+      const uint32_t tK = std::min<uint32_t>(C, s.k - (K - 1) * C), g0 = (K - 1) * C;
+      bool anyK = false;
+      for (uint32_t q = 0; q < tK; q++) anyK |= !s.present[g0 + q];
+      if (!anyK) continue;
+      const std::vector<Layer> fl = fft_layers(C, tK, static_cast<uint64_t>(K) * C);
+      // backward: positions needed (A layers), then register rows needed (B layers)
+      std::vector<uint8_t> need(C, 0);
+      for (uint32_t q = 0; q < tK; q++) need[q] = !s.present[g0 + q];
+      std::map<std::pair<size_t, size_t>, bool> emit;  // (layer, butterfly) -> emitted
+      for (size_t li = fl.size(); li-- > 0;) {
+        if (!P.inA(fl[li].bit)) continue;
+        for (size_t bi = fl[li].bf.size(); bi-- > 0;) {
+          const Bf &b = fl[li].bf[bi];
+          const bool e = need[b.x] || need[b.y];
+          emit[{li, bi}] = e;
+          if (e) need[b.x] = need[b.y] = 1;
+        }
+      }
+      std::vector<uint8_t> nB(8, 0);  // rows the B phase must deliver
+      for (uint32_t q = 0; q < C; q++)
+        if (need[q]) nB[P.regB(q)] = 1;
+      std::vector<uint8_t> nb = nB;
+      for (size_t li = fl.size(); li-- > 0;) {
+        if (P.inA(fl[li].bit)) continue;
+        for (size_t bi = fl[li].bf.size(); bi-- > 0;) {
+          const Bf &b = fl[li].bf[bi];
+          if (P.waveB(b.x) != 0) continue;
+          const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+          const bool e = nb[tx] || nb[ty];
+          emit[{li, bi}] = e;
+          if (e) nb[tx] = nb[ty] = 1;
+        }
+      }
+      const bool last = K == last_blk;
+      auto bn = [&](uint32_t t) { return last ? cname(t) : bname(t); };
+      if (last && pfu) emit_next_unit_loads();
+      o << "  __builtin_amdgcn_sched_barrier(0);\n  {  // data block " << K << ": FFT(size " << C << ", trunc " << tK
+        << ", skew_delta " << K * C << ")\n";
+      g.ops = &g.st->ops_b;
+      bool zb[8];
+      for (uint32_t t = 0; t < 8; t++) {
+        zb[t] = za[t] || !nb[t];
+        if (!zb[t] && !last) g.copy(Gen::regs(bname(t)), Gen::regs(cname(t)));
+      }
+      for (size_t li = 0; li < fl.size(); li++) {
+        if (P.inA(fl[li].bit)) continue;
+        for (size_t bi = 0; bi < fl[li].bf.size(); bi++) {
+          const Bf &b = fl[li].bf[bi];
+          if (P.waveB(b.x) != 0 || !emit[{li, bi}]) continue;
+          const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
+          g.butterfly(bn(tx), zb[tx], bn(ty), zb[ty], false, P.get_tw(b.log_m));
+        }
+      }
+      std::vector<uint8_t> rA(8, 0);
+      for (uint32_t q = 0; q < C; q++)
+        if (need[q] && !zb[P.regB(q)]) rA[P.regA(q)] = 1;
+      o << "  {\n  LQ();\n";
+      for (uint32_t t = 0; t < 8; t++)
+        if (nB[t] && !zb[t]) lds_write("w", t << P.WB, Gen::regs(bn(t)));
+      o << "  BAR();\n";
+      for (uint32_t r = 0; r < 8; r++)
+        if (rA[r]) lds_read("(w * 8u)", r, Gen::regs(wname(r)));
+      o << "  BAR();\n  }\n";
+      // A layers and the erased shards' outputs, per wave
+      bool firstw = true;
+      for (uint32_t w = 0; w < NW; w++) {
+        bool anyw = false;
+        for (uint32_t r = 0; r < 8; r++) {
+          const uint32_t q = P.posA(w, r);
+          anyw |= q < tK && !s.present[g0 + q];
+        }
+        if (!anyw) continue;
+        o << "  " << (firstw ? "if" : "else if") << " (w == " << w << "u) {\n";
+        firstw = false;
+        g.ops = &g.st->ops_a;
+        bool z[8];
+        for (uint32_t r = 0; r < 8; r++) z[r] = zb[P.regB(P.posA(w, r))] || !need[P.posA(w, r)];
+        for (size_t li = 0; li < fl.size(); li++) {
+          if (!P.inA(fl[li].bit)) continue;
+          for (size_t bi = 0; bi < fl[li].bf.size(); bi++) {
+            const Bf &b = fl[li].bf[bi];
+            if (P.waveA(b.x) != w || !emit[{li, bi}]) continue;
+            const uint32_t rx = P.regA(b.x), ry = P.regA(b.y);
+            g.butterfly(wname(rx), z[rx], wname(ry), z[ry], false, P.get_tw(b.log_m));
+          }
+        }
+        g.ops = &g.st->ops_io;
+        for (uint32_t r = 0; r < 8; r++) {
+          const uint32_t q = P.posA(w, r), gi = g0 + q;
+          if (q >= tK || s.present[gi]) continue;
+          const auto W = Gen::regs(wname(r));
+          if (z[r] || cg_log[gi] > kModulus) {
+            for (int i = 0; i < 8; i++) o << "  " << W[i] << " = 0u;\n";
+          } else {
+            cmul(W, cg_log[gi]);
+            g.basis_change(W);
+          }
+          o << "  __builtin_amdgcn_sched_barrier(0);\n  { u32 X[8] = {";
+          for (int i = 0; i < 8; i++) o << W[i] << (i < 7 ? ", " : "};\n");
+          o << "  v4 a, b; unplanes2(X, a, b);\n  STB(a, RO, uo, " << out_row[gi] << "u * sbl); STB(b, RO1, uo1, "
+            << out_row[gi] << "u * sbl); }\n";
+        }
+        o << "  }\n";
+      }
+      o << "  }\n";
+    }
+  } else if (tail) {
     // ---- decode tail (Spec::decode): w_p = L_p (rec_p ^ Enc_p) for the
     // rows R (layout A), a = IFFT(size C, trunc m, skew 0) (A then B), and per data block K
     // with an erasure: FFT(a, size C, trunc t_K, skew KC) (B then A), x_g = (L'_g beta_K) y_q
-    const uint32_t dwm = dyn_store_word(P) + 2, mko = decode_mask_offset(s);
+    const uint32_t mko = decode_mask_offset(s);
     g.ops = &g.st->ops_io;
-    o << "  {  // syndromes of the rows R times the locator (one code path, runtime scalars)\n"
-      << "  const u32 ub0 = DMc[" << dwm + 1 << "], ub1 = DMc[" << dwm + 2 << "];\n";
-    for (uint32_t r = 0; r < 8; r++)
-      o << "  const u32 pd" << r << " = w * 8u + " << r << "u;\n  const bool us" << r << " = ((pd" << r
-        << " < 32u ? ub0 >> pd" << r << " : ub1 >> (pd" << r << " - 32u)) & 1u) != 0u;\n  const v4 ra" << r
-        << " = LDB(us" << r << " ? RR : RZ, uo, pd" << r << " * sbl), rb" << r << " = LDB(us" << r
-        << " ? RR1 : RZ, uo1, pd" << r << " * sbl);\n";
+    o << "  {  // syndromes of the rows R times the locator (one code path, runtime scalars)\n";
+    if (old_order) emit_rec_loads();
     for (uint32_t r = 0; r < 8; r++) {
       const auto W = Gen::regs(wname(r));
       o << "  if (us" << r << ") {\n  u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q);\n";
@@ -981,20 +1314,25 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         for (const Bf &b : it->bf)
           if (nd[b.x] || nd[b.y]) nd[b.x] = nd[b.y] = 1;
       }
+      // the last block transforms a in place (its last use), and the next unit's leading
+      // positions are loaded before it (a's registers free up there)
+      const bool last = K == nblk && !old_order;
+      auto bn = [&](uint32_t t) { return last ? cname(t) : bname(t); };
+      if (last && pfu) emit_next_unit_loads();
       o << "  __builtin_amdgcn_sched_barrier(0);\n  if ((DMc[" << dwm << "] >> " << K << "u) & 1u) {  // data block " << K
         << ": FFT(size " << C << ", trunc " << tK << ", skew_delta " << K * C << ")\n";
       g.ops = &g.st->ops_b;
       bool zb[8];
       for (uint32_t t = 0; t < 8; t++) {
         zb[t] = za[t];
-        if (!za[t]) g.copy(Gen::regs(bname(t)), Gen::regs(cname(t)));
+        if (!za[t] && !last) g.copy(Gen::regs(bname(t)), Gen::regs(cname(t)));
       }
       for (const Layer &L : fl) {
         if (P.inA(L.bit)) continue;
         for (const Bf &b : L.bf) {
           if (P.waveB(b.x) != 0) continue;
           const uint32_t tx = P.regB(b.x), ty = P.regB(b.y);
-          g.butterfly(bname(tx), zb[tx], bname(ty), zb[ty], false, P.get_tw(b.log_m));
+          g.butterfly(bn(tx), zb[tx], bn(ty), zb[ty], false, P.get_tw(b.log_m));
         }
       }
       std::vector<uint8_t> nB(8, 0), rA(8, 0);
@@ -1005,7 +1343,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         }
       o << "  {\n  LQ();\n";
       for (uint32_t t = 0; t < 8; t++)
-        if (nB[t] && !zb[t]) lds_write("w", t << P.WB, Gen::regs(bname(t)));
+        if (nB[t] && !zb[t]) lds_write("w", t << P.WB, Gen::regs(bn(t)));
       o << "  BAR();\n";
       for (uint32_t r = 0; r < 8; r++)
         if (rA[r]) lds_read("(w * 8u)", r, Gen::regs(wname(r)));
@@ -1087,11 +1425,16 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
-  std::string k = "fft3:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":" +
+  std::string k = "fft4:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":d" +
+                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":v" + std::to_string(rmul_vload()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
                   (s.dyn ? "dyn:" : "") + (s.decode ? "dec:" : "") + (s.blocked ? "blk:" : "");
+  if (!s.present.empty()) {
+    k += "pat:";
+    for (uint8_t b : s.present) k.push_back(b ? '1' : '0');
+  }
   for (uint8_t b : s.skip) k.push_back(static_cast<char>('0' + b));
   k.push_back(':');
   for (uint8_t b : s.out_mode) k.push_back(static_cast<char>('0' + b));
@@ -1103,7 +1446,7 @@ std::string kernel_name(const Spec &s) {
   for (unsigned char c : cache_key(s)) h = (h ^ c) * 1099511628211ull;
   char name[96];
   std::snprintf(name, sizeof name, "rs_fft_%s_k%u_m%u_%016llx",
-                s.inverse ? "inverse" : s.decode ? "decode" : "encode", s.k, s.m,
+                s.inverse ? "inverse" : s.decode ? (s.present.empty() ? "decode" : "pdecode") : "encode", s.k, s.m,
                 static_cast<unsigned long long>(h));
   return name;
 }
@@ -1265,11 +1608,12 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
                   uint8_t *out, uint64_t os, uint64_t sb, uint64_t n_stripes, hipStream_t st, const uint32_t *dmask,
                   uint32_t dmask_words, bool shared_mask) {
   if (n_stripes == 0) return hipSuccess;
-  if (!supports(s.k, s.m, sb, s.dyn) || pieces(sb) != s.pieces || (s.inverse && !supports_inverse(s.k, s.m, sb)))
+  if (!supports(s.k, s.m, sb, s.dyn || s.decode) || pieces(sb) != s.pieces ||
+      (s.inverse && !supports_inverse(s.k, s.m, sb)))
     return hipErrorInvalidValue;
   if (s.dyn && (s.pieces != 1 || !dmask || dmask_words < (s.decode ? decode_block_words(s) : dyn_mask_words(s))))
     return hipErrorInvalidValue;
-  if (s.decode && (!s.dyn || s.inverse || s.flags || !rec)) return hipErrorInvalidValue;
+  if (s.decode && ((!s.dyn && s.present.empty()) || s.inverse || s.flags || !rec)) return hipErrorInvalidValue;
   const uint32_t C = static_cast<uint32_t>(ceil_pow2(s.m));
   static std::mutex mu;
   static std::map<int, int> cus;

@@ -61,6 +61,11 @@ struct Spec {
   // workgroup b walks units [b per, (b + 1) per) instead of b, b + grid, ...: one stripe's
   // units in a row (per-stripe decode blocks stay in the scalar cache)
   bool blocked = false;
+  // fused reconstruct of ONE erasure pattern (decode without dyn; k + m flags): the pattern
+  // compiled in — the locator scalars as constant multiplies, the rows R, the erased data
+  // positions, the output rows and the blocks static, butterflies no erased shard needs
+  // pruned. No decode block.
+  std::vector<uint8_t> present;
 };
 // u32 words of a stripe's mask block (Spec::dyn): bit p of words [0, w - 2) = data shard
 // p read as zero, bit q of the last 2 words = parity row q stored

@@ -33,8 +33,27 @@ namespace host {
 
 // ------------------------------------------------------------ errors (rs_common.cpp)
 int fail(int status, const std::string &msg);  // sets rs_last_error()
-int hip_fail(hipError_t e, const char *what);
+int hip_fail(hipError_t e, const char *what);   // hipErrorOutOfMemory -> RS_ERR_OUT_OF_MEMORY
 const char *last_error();
+
+// Allocation-failure injection (rs_debug_fail_alloc; the reference's
+// checkAllAllocationFailures, tests.zig:131-156): every allocation the library makes
+// — plan objects (alloc_point, throws std::bad_alloc), device, async-pool and pinned
+// buffers (the wrappers, hipErrorOutOfMemory) — is counted, and the armed one fails.
+bool alloc_fails();
+void alloc_point();
+hipError_t dev_malloc(void **p, size_t bytes);
+hipError_t dev_malloc_async(void **p, size_t bytes, hipStream_t s);
+hipError_t pinned_malloc(void **p, size_t bytes);
+int64_t arm_alloc_failure(int64_t n);  // returns the allocations counted since the last call
+// Drop every cache that holds device or pinned memory (plans, tables, staging rings,
+// one-shot contexts); compiled kernels stay loaded (rs_debug_release_caches).
+void release_plans();      // rs_plans.cpp (+ twiddles, rs_common.cpp)
+void release_patterns();   // rs_patterns.cpp
+void release_lowrate();    // rs_lowrate.cpp
+void release_oneshot();    // rs_oneshot.cpp
+size_t oneshot_pooled();   // one-shot contexts idle in the pool
+void release_host_rings(); // rs_host_batch.cpp
 
 #define HIP_TRY(expr)                               \
   do {                                              \
@@ -152,6 +171,9 @@ struct DecodePlan {
   // decode block (rows R, locator masks, output rows); the kernel is per code
   std::shared_ptr<DevBuf> fdec_blk;
   uint32_t fdec_words = 0;
+  // the same reconstruct with this pattern compiled in (fftnet::Spec::present; background
+  // compile): the steady state of a wide-code pattern unless a direct network beats it
+  std::shared_ptr<FftSlot> pdec;
   // a pattern's first use builds only the fused block (no network spec, no tables: the
   // host GF(2) algebra of those takes 10-40 ms); where a network would beat the fused
   // kernel, its next use has the full plan built on the background worker
@@ -203,6 +225,7 @@ struct PlanCache {
     return v;
   }
   size_t size() const { return m.size(); }
+  void clear() { m.clear(); }  // g_plan_mu held
 };
 
 extern std::mutex g_plan_mu;
@@ -276,6 +299,8 @@ const jit::Kernel *wps_solve_kernel(WpsSlot &ws);
 // (default) unless the pattern's e x e network is loaded
 int fdec_mode();
 bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags);
+// RS_AMD_PDEC (default on): a reused wide-code pattern gets its pattern-compiled fused kernel
+bool pdec_enabled();
 // exp, log, log_walsh in HBM (384 KiB per device)
 int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw);
 

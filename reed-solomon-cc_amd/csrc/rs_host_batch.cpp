@@ -47,7 +47,7 @@ struct Pipeline {
     for (int j = 0; j < 3; j++) cap[j] = std::max(cap[j], bytes[j]);
     for (int i = 0; i < want; i++)
       for (int j = 0; j < 3; j++)
-        if (cap[j]) HIP_TRY(hipMalloc(&buf[i][j], cap[j]));
+        if (cap[j]) HIP_TRY(dev_malloc(&buf[i][j], cap[j]));
     slots = want;
     return RS_OK;
   }
@@ -98,8 +98,26 @@ struct Pipelines {
   }
 };
 
-
 }  // namespace
+
+void rs::host::release_host_rings() {
+  std::lock_guard<std::mutex> lk(g_pipe_mu);
+  for (auto &kv : g_pipes) {
+    Pipeline &p = *kv.second;
+    std::lock_guard<std::mutex> pk(p.mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first);
+    for (int i = 0; i < Pipeline::kMaxSlots; i++)
+      for (int j = 0; j < 3; j++) {
+        if (p.buf[i][j]) (void)hipFree(p.buf[i][j]);
+        p.buf[i][j] = nullptr;
+      }
+    p.slots = 0;
+    for (int j = 0; j < 3; j++) p.cap[j] = 0;
+    (void)hipSetDevice(cur);
+  }
+}
 
 extern "C" {
 

@@ -49,6 +49,12 @@ PlanCache<LowDecodePlan> g_low_dec;  // a W = 65536 plan holds 13 MB of HBM: pla
 
 }  // namespace
 
+void release_lowrate() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  g_low_enc.clear();
+  g_low_dec.clear();
+}
+
 void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
   (void)flags;  // corrected multiply (quirks have no low-rate meaning)
   ns.role = "encode_low";
@@ -141,6 +147,7 @@ int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, std::share
     std::lock_guard<std::mutex> lk(g_plan_mu);
     if ((out = g_low_enc.find(key))) return RS_OK;
   }
+  alloc_point();
   auto p = std::make_shared<LowEncodePlan>();
   const uint64_t C = ceil_pow2(k);
   p->C = static_cast<uint32_t>(C);
@@ -174,6 +181,7 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
     std::lock_guard<std::mutex> lk(g_plan_mu);
     if ((out = g_low_dec.find(key))) return RS_OK;
   }
+  alloc_point();
   auto p = std::make_shared<LowDecodePlan>();
   const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end);
   p->W = static_cast<uint32_t>(W);
@@ -221,7 +229,7 @@ template <class F>
 int in_scratch_slices(uint64_t n, uint64_t per_stripe_bytes, hipStream_t s, F &&launch) {
   const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n, kScratchCap / per_stripe_bytes));
   void *scratch = nullptr;
-  HIP_TRY(hipMallocAsync(&scratch, per * per_stripe_bytes, s));
+  HIP_TRY(dev_malloc_async(&scratch, per * per_stripe_bytes, s));
   hipError_t e = hipSuccess;
   for (uint64_t s0 = 0; e == hipSuccess && s0 < n; s0 += per)
     e = launch(s0, std::min(per, n - s0), static_cast<uint8_t *>(scratch));

@@ -41,6 +41,7 @@ int oneshot_acquire(int dev, size_t bytes, OneShot **out) {
       }
   }
   if (!c) {
+    alloc_point();
     c = new OneShot;
     c->dev = dev;
     hipError_t e = hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking);
@@ -56,8 +57,8 @@ int oneshot_acquire(int dev, size_t bytes, OneShot **out) {
     if (c->d) (void)hipFree(c->d);
     c->h = c->d = nullptr;
     c->bytes = 0;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&c->h), nb, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&c->d), nb);
+    hipError_t e = pinned_malloc(reinterpret_cast<void **>(&c->h), nb);
+    if (e == hipSuccess) e = dev_malloc(reinterpret_cast<void **>(&c->d), nb);
     if (e != hipSuccess) {
       if (c->h) (void)hipHostFree(c->h);
       c->h = nullptr;
@@ -88,6 +89,29 @@ struct OneShotLease {  // drains the stream and returns the context on every exi
 
 inline size_t align256(size_t x) { return (x + 255) & ~static_cast<size_t>(255); }
 }  // namespace
+
+void rs::host::release_oneshot() {
+  std::vector<OneShot *> all;
+  {
+    std::lock_guard<std::mutex> lk(g_oneshot_mu);
+    all.swap(g_oneshot_free);  // contexts leased by calls in flight come back later
+  }
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (OneShot *c : all) {
+    (void)hipSetDevice(c->dev);
+    if (c->h) (void)hipHostFree(c->h);
+    if (c->d) (void)hipFree(c->d);
+    if (c->s) (void)hipStreamDestroy(c->s);
+    delete c;
+  }
+  (void)hipSetDevice(cur);
+}
+
+size_t rs::host::oneshot_pooled() {
+  std::lock_guard<std::mutex> lk(g_oneshot_mu);
+  return g_oneshot_free.size();
+}
 
 extern "C" {
 
@@ -181,6 +205,7 @@ int rs_encoder_new(uint64_t k, uint64_t m, size_t sb, rs_encoder **out) {
     int st = check_codec(k, m, sb);  // root.zig:100-103
     if (st) return st;
     try {
+      alloc_point();
       rs_encoder *e = new rs_encoder;
       e->k = k;
       e->m = m;
@@ -249,6 +274,7 @@ int rs_decoder_new(uint64_t k, uint64_t m, size_t sb, rs_decoder **out) {
     int st = check_codec(k, m, sb);  // root.zig:198-201
     if (st) return st;
     try {
+      alloc_point();
       rs_decoder *d = new rs_decoder;
       d->k = k;
       d->m = m;
@@ -331,9 +357,9 @@ static int engine_transform(uint8_t *shards, uint64_t count, size_t sb, uint64_t
   if (inverse) push_ifft_tabs(tabs, size, sd, flags & RS_FLAG_QUIRK_D1);
   else push_fft_tabs(tabs, size, sd, flags & RS_FLAG_QUIRK_D1);
   DevMem dt, dw;
-  HIP_TRY(hipMalloc(&dt.p, std::max<size_t>(16, tabs.size() * sizeof(RsTab))));
+  HIP_TRY(dev_malloc(&dt.p, std::max<size_t>(16, tabs.size() * sizeof(RsTab))));
   if (!tabs.empty()) HIP_TRY(hipMemcpy(dt.p, tabs.data(), tabs.size() * sizeof(RsTab), hipMemcpyHostToDevice));
-  HIP_TRY(hipMalloc(&dw.p, count * sb));
+  HIP_TRY(dev_malloc(&dw.p, count * sb));
   HIP_TRY(hipMemcpy(dw.p, shards, count * sb, hipMemcpyHostToDevice));
   HIP_TRY(launch_engine_fft(static_cast<uint8_t *>(dw.p), sb, pos, size, trunc, static_cast<const RsTab *>(dt.p),
                             inverse, nullptr));
@@ -366,9 +392,9 @@ int rs_engine_mul_scalar(uint8_t *chunks, size_t bytes, uint16_t log_m, uint32_t
     if ((st = current_device(&dev))) return st;
     const RsTab t = make_tab(log_m, flags & RS_FLAG_QUIRK_D1);
     DevMem dt, dw;
-    HIP_TRY(hipMalloc(&dt.p, sizeof t));
+    HIP_TRY(dev_malloc(&dt.p, sizeof t));
     HIP_TRY(hipMemcpy(dt.p, &t, sizeof t, hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&dw.p, bytes));
+    HIP_TRY(dev_malloc(&dw.p, bytes));
     HIP_TRY(hipMemcpy(dw.p, chunks, bytes, hipMemcpyHostToDevice));
     HIP_TRY(launch_mul_scalar(static_cast<uint8_t *>(dw.p), bytes, static_cast<const RsTab *>(dt.p), nullptr));
     HIP_TRY(hipMemcpy(chunks, dw.p, bytes, hipMemcpyDeviceToHost));

@@ -64,6 +64,11 @@ int fdec_mode() {
   return 2;
 }
 
+bool pdec_enabled() {
+  const char *e = std::getenv("RS_AMD_PDEC");
+  return fdec_mode() != 1 && !(e && std::strcmp(e, "0") == 0);
+}
+
 // corrected multiply only (under D1 the literal decode is no inverse of the encode), and
 // no code whose D2 encode drops a chunk (its parity is no codeword, so the result would
 // depend on which recovery rows are read; root.zig:268-335 reads all of them)
@@ -114,6 +119,7 @@ int psyn_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<P
       return RS_OK;
     }
   }
+  alloc_point();
   auto p = std::make_shared<PsynPlan>();
   jit::NetSpec map;
   encode_map(k, m, flags & RS_FLAG_QUIRK_D2, map);
@@ -187,6 +193,13 @@ bool psyn_enabled(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
 
 }  // namespace
 
+void rs::host::release_patterns() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  g_dev_tables.clear();
+  g_wps.clear();
+  g_psyn_plans.clear();
+}
+
 extern "C" {
 
 const char *rs_patterns_kernel_name(uint64_t k, uint64_t m, size_t sb, uint32_t max_e, uint32_t flags) {
@@ -231,7 +244,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       const uint64_t psb = (sb + 63) / 64 * 64, rows = k + m + max_e;
       const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kTailSliceBytes / (rows * psb)));
       void *buf = nullptr;
-      HIP_TRY(hipMallocAsync(&buf, cap * rows * psb, s));
+      HIP_TRY(dev_malloc_async(&buf, cap * rows * psb, s));
       uint8_t *po = static_cast<uint8_t *>(buf), *pr = po + cap * k * psb, *pout = pr + cap * m * psb;
       const uint8_t *O = static_cast<const uint8_t *>(d_original), *Rc = static_cast<const uint8_t *>(d_recovery);
       uint8_t *Out = static_cast<uint8_t *>(d_restored);
@@ -274,7 +287,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
         const uint32_t mo = psyn::max_out(static_cast<uint32_t>(k), static_cast<uint32_t>(m));
         const uint32_t pdw = psyn::plan_dwords(static_cast<uint32_t>(k), static_cast<uint32_t>(m));
         void *blk = nullptr;
-        HIP_TRY(hipMallocAsync(&blk, n_stripes * pdw * sizeof(uint32_t), s));
+        HIP_TRY(dev_malloc_async(&blk, n_stripes * pdw * sizeof(uint32_t), s));
         hipError_t e = launch_psyn_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m), mo,
                                         max_e, n_stripes, static_cast<const uint16_t *>(pp->G->p), dexp, dlog,
                                         static_cast<uint32_t *>(blk), pdw, d_status, s);
@@ -310,7 +323,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
         const uint64_t per_bytes = static_cast<uint64_t>(words) * 4 + (k + m) + W * 2;
         const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, (1ull << 30) / per_bytes));
         void *tmp = nullptr;
-        HIP_TRY(hipMallocAsync(&tmp, per * per_bytes + 256, s));
+        HIP_TRY(dev_malloc_async(&tmp, per * per_bytes + 256, s));
         uint32_t *blk = static_cast<uint32_t *>(tmp);
         uint16_t *logs = reinterpret_cast<uint16_t *>(blk + per * words);
         uint8_t *trimmed = reinterpret_cast<uint8_t *>(logs + per * W);
@@ -348,8 +361,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
         const uint32_t dmw = fftnet::dyn_mask_words(*fs), pw = dmw + 2 + 64 + 64 * cs;
         const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (m * sb)));
         void *blk = nullptr, *scratch = nullptr;
-        HIP_TRY(hipMallocAsync(&blk, n_stripes * pw * sizeof(uint32_t), s));
-        hipError_t e = hipMallocAsync(&scratch, per * m * sb, s);
+        HIP_TRY(dev_malloc_async(&blk, n_stripes * pw * sizeof(uint32_t), s));
+        hipError_t e = dev_malloc_async(&scratch, per * m * sb, s);
         if (e == hipSuccess)
           e = launch_wps_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
                               static_cast<uint32_t>(std::min<uint64_t>(max_e, m)), n_stripes, static_cast<const uint16_t *>(pp->G->p), dexp, dlog, static_cast<uint32_t *>(blk),
@@ -383,7 +396,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     //                  [| trimmed present rows, matrix path]
     const uint64_t per = W * (2 + 2 * sizeof(RsTab) + 8);
     void *tmp = nullptr;
-    HIP_TRY(hipMallocAsync(&tmp, n_stripes * per + (use_matrix ? n_stripes * (k + m) : 0) + 256, s));
+    HIP_TRY(dev_malloc_async(&tmp, n_stripes * per + (use_matrix ? n_stripes * (k + m) : 0) + 256, s));
     if (use_matrix) {  // evaluate the erasure locator for exactly the k inputs the matrix uses
       uint8_t *trimmed = static_cast<uint8_t *>(tmp) + n_stripes * per;
       hipError_t e = launch_trim_present(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
@@ -417,7 +430,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       const uint64_t nk = n_stripes * k;
       void *mt = nullptr;
       const uint64_t img_bytes = nk * max_e * 16 * sizeof(uint16_t), tab_bytes = nk * max_e * sizeof(RsTab);
-      e = hipMallocAsync(&mt, tab_bytes + img_bytes + nk * 4 + n_stripes * 4 + 256, s);
+      e = dev_malloc_async(&mt, tab_bytes + img_bytes + nk * 4 + n_stripes * 4 + 256, s);
       if (e == hipSuccess) {
         RsTab *mtabs = static_cast<RsTab *>(mt);
         uint16_t *images = reinterpret_cast<uint16_t *>(static_cast<uint8_t *>(mt) + tab_bytes);
@@ -482,7 +495,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     } else {
       const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (W * sb)));
       void *scratch = nullptr;
-      e = hipMallocAsync(&scratch, cap * W * sb, s);
+      e = dev_malloc_async(&scratch, cap * W * sb, s);
       for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += cap) {
         DecodeArgs b = a;
         b.orig += s0 * orig_stride;

@@ -9,6 +9,12 @@ namespace host {
 PlanCache<EncodePlan> g_enc_plans;
 PlanCache<DecodePlan> g_dec_plans;
 
+void release_plans() {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  g_enc_plans.clear();
+  g_dec_plans.clear();
+}
+
 // The encode as a k -> m map of GF(2)-linear 16x16 maps: images of every basis
 // symbol of every data shard through Encoder.encode (root.zig:136-173).
 void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns) {
@@ -92,6 +98,7 @@ int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared
   std::vector<RsTab> tabs;
   for (size_t j = 0; j < truncs.size(); j++) push_ifft_tabs(tabs, C, (j + 1) * C, d1);
   push_fft_tabs(tabs, C, 0, d1);
+  alloc_point();
   auto plan = std::make_shared<EncodePlan>();
   int st = upload(tabs.data(), tabs.size() * sizeof(RsTab), dev, plan->buf);
   if (st) return st;
@@ -222,7 +229,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
                     std::to_string(jit::enabled() && jit::shard_ok(sb)) + "/" +
                     std::to_string(fft_enabled() && fftnet::supports(k, m, sb)) + "/" +
                     std::to_string(jit::max_blocks()) + "/" + std::to_string(jit::max_async_blocks()) + "/" +
-                    std::to_string(fdec_mode()) + "/" + std::to_string(fdec_supports(k, m, sb, flags)) + "/";
+                    std::to_string(fdec_mode()) + "/" + std::to_string(fdec_supports(k, m, sb, flags)) + "/" +
+                    std::to_string(pdec_enabled()) + "/";
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   std::shared_ptr<DecodePlan> lite;
@@ -244,6 +252,7 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   const bool every_lost = e == k && present_count == m;  // the inverse form's case stays on the full plan
   if (!lite && !full && e > 0 && !every_lost && m <= 64 && fdec_supports(k, m, sb, flags) &&
       (mode == "auto" || mode == "net")) {
+    alloc_point();
     auto plan = std::make_shared<DecodePlan>();
     fftnet::Spec ds;
     ds.k = static_cast<uint32_t>(k);
@@ -275,8 +284,13 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   // e x e map for e >= 3/4 m (55 losses 6.6 vs 6.9 ms; 20 losses the fused kernel wins, 4.9
   // vs 6.2 ms; profiles/r03/fdec/). The others skip the host plan algebra (10-40 ms) and
   // the background compile for good.
-  const bool syn_wins = syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
-  if (lite && !full && !use_net && !use_net_async && !syn_wins) {
+  // a reused wide-code pattern gets the fused kernel with the pattern compiled in (constant
+  // locator multiplies: no scalar-loaded masks); it replaces the syndrome
+  // path's e x e network, and a direct network (few losses) stays ahead of it
+  const bool pdec_on = e > 0 && !every_lost && m <= 64 && pdec_enabled() && fdec_supports(k, m, sb, flags) &&
+                       (mode == "auto" || mode == "net");
+  const bool syn_wins = !pdec_on && syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
+  if (lite && !full && !use_net && !use_net_async && !syn_wins && !pdec_on) {
     out = lite;
     return RS_OK;
   }
@@ -288,19 +302,25 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
       // rs_net_wait returns only once the pattern's steady-state kernel is loaded)
       if (!jit::run_host_job("plan:" + key, [dev, k, m, sb, flags, pres] {
             std::shared_ptr<DecodePlan> p;
-            if (get_decode_plan(dev, k, m, sb, flags, pres.data(), p, 2) == RS_OK && p && p->net) queue_net(*p->net, sb);
+            if (get_decode_plan(dev, k, m, sb, flags, pres.data(), p, 2) != RS_OK || !p) return;
+            if (p->net) queue_net(*p->net, sb);
+            if (p->pdec) {
+              const fftnet::Spec *fs = nullptr;
+              (void)fft_kernel(*p->pdec, sb, &fs);
+            }
           }))
         lite->upgrading = false;
     }
     return RS_OK;
   }
-  const bool use_syn = !use_net && !use_net_async && syndrome_pick(k, m, e, flags, sb, mode);
+  const bool use_syn = !use_net && !use_net_async && !pdec_on && syndrome_pick(k, m, e, flags, sb, mode);
   if (use_syn) kind = e <= kMatrixMaxOut ? 1 : 2;
   // the syndromes' e x e map as a network too (its table kernel stays the fallback)
   const bool syn_net = use_syn && (mode == "auto" || mode == "net" || mode == "syndrome") && jit::enabled() &&
                        jit::supports_async(static_cast<uint32_t>(e), static_cast<uint32_t>(e), sb);
   const bool use_matrix = kind != 0;
 
+  alloc_point();
   auto plan = std::make_shared<DecodePlan>();
   plan->work = static_cast<uint32_t>(W);
   plan->chunk = static_cast<uint32_t>(C);
@@ -319,6 +339,15 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     plan->inv_fft->spec.inverse = true;
   }
 
+  if (pdec_on) {
+    plan->pdec = std::make_shared<FftSlot>();
+    plan->pdec->async = true;
+    fftnet::Spec &ps = plan->pdec->spec;
+    ps.k = static_cast<uint32_t>(k);
+    ps.m = static_cast<uint32_t>(m);
+    ps.decode = true;
+    ps.present.assign(present, present + k + m);
+  }
   // the fused FFT reconstruct's block for this pattern (wide codes): the
   // form every pattern runs until a network compiled for it is loaded
   if (lite) {
@@ -538,6 +567,31 @@ int rs_fft_decode_compile_check(uint64_t k, uint64_t m, double *compile_ms, uint
     spec.k = static_cast<uint32_t>(k);
     spec.m = static_cast<uint32_t>(m);
     spec.dyn = spec.decode = true;
+    std::string err;
+    size_t bytes = 0;
+    if (!fftnet::compile_check(spec, err, compile_ms, &bytes)) return fail(RS_ERR_DEVICE, err);
+    if (code_bytes) *code_bytes = bytes;
+    return RS_OK;
+  });
+}
+
+int rs_fft_pdecode_compile_check(uint64_t k, uint64_t m, const uint8_t *present, double *compile_ms,
+                                 uint64_t *code_bytes) {
+  return guarded([&]() -> int {
+    int st = check_codec(k, m, fftnet::kUnitBytes);
+    if (st) return st;
+    if (!present) return fail(RS_ERR_INVALID_ARGUMENT, "present == NULL");
+    if (!fftnet::supports(k, m, fftnet::kUnitBytes, true)) return fail(RS_ERR_INVALID_ARGUMENT, "no FFT kernel form");
+    uint64_t e = 0, have = 0;
+    for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+    for (uint64_t i = 0; i < m; i++) have += present[k + i] ? 1 : 0;
+    if (have < e) return fail(RS_ERR_NOT_ENOUGH_SHARDS, "fewer than original_count shards present");
+    if (e == 0) return fail(RS_ERR_INVALID_ARGUMENT, "nothing erased");
+    fftnet::Spec spec;
+    spec.k = static_cast<uint32_t>(k);
+    spec.m = static_cast<uint32_t>(m);
+    spec.decode = true;
+    spec.present.assign(present, present + k + m);
     std::string err;
     size_t bytes = 0;
     if (!fftnet::compile_check(spec, err, compile_ms, &bytes)) return fail(RS_ERR_DEVICE, err);

@@ -90,12 +90,15 @@ def lib():
         "rs_net_wait": (C.c_int, []),
         "rs_reconstruct_warm": (C.c_int, [u64, u64, sz, vp, u32]),
         "rs_last_kernels": (C.c_char_p, []),
+        "rs_debug_fail_alloc": (C.c_int64, [C.c_int64]),
+        "rs_debug_release_caches": (C.c_int, [vp]),
         "rs_jit_stats": (C.c_int, [vp, vp, vp]),
         "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
         "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
         "rs_patterns_kernel_name": (C.c_char_p, [u64, u64, sz, u32, u32]),
         "rs_fft_selftest": (C.c_int, [u64, u64, u32, vp, C.c_int, vp]),
         "rs_fft_decode_compile_check": (C.c_int, [u64, u64, vp, vp]),
+        "rs_fft_pdecode_compile_check": (C.c_int, [u64, u64, vp, vp, vp]),
         "rs_fft_decode_selftest": (C.c_int, [u64, u64, u32, C.c_int, vp]),
         "rs_lowrate_selftest": (C.c_int, [u64, u64, C.c_int, u64, vp]),
         "rs_engine_fft": (C.c_int, [vp, u64, sz, u64, u64, u64, u64, u32]),
@@ -400,6 +403,14 @@ def fft_decode_compile_check(k, m) -> dict:
     return {"compile_ms": ms.value, "code_bytes": b.value}
 
 
+def fft_pdecode_compile_check(k, m, present) -> dict:
+    """Generate + hipRTC-compile the fused FFT reconstruct with one pattern compiled in (no device)."""
+    ms, b = C.c_double(0), C.c_uint64(0)
+    pres = (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
+    _check(lib().rs_fft_pdecode_compile_check(k, m, pres, C.byref(ms), C.byref(b)))
+    return {"compile_ms": ms.value, "code_bytes": b.value}
+
+
 def fft_decode_selftest(k, m, erased, trials=8) -> int:
     """Host check of the fused FFT reconstruct's schedule: wrong restored symbols."""
     bad = C.c_uint64(0)
@@ -418,6 +429,20 @@ def reconstruct_warm(k, m, shard_bytes, present, flags: int = FLAG_CORRECTED) ->
     launch compiled and loaded), blocking; include/reedsol.h rs_reconstruct_warm."""
     pres = (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
     _check(lib().rs_reconstruct_warm(k, m, shard_bytes, pres, flags))
+
+
+def debug_fail_alloc(n: int) -> int:
+    """Arm allocation-failure injection (the n-th allocation fails; n < 0 disarms);
+    returns the allocations counted since the previous call (include/reedsol.h)."""
+    return int(lib().rs_debug_fail_alloc(n))
+
+
+def debug_release_caches() -> int:
+    """Drop every plan / table / staging cache holding device or pinned memory; returns the
+    one-shot contexts left pooled."""
+    n = C.c_uint64()
+    _check(lib().rs_debug_release_caches(C.byref(n)))
+    return n.value
 
 
 def last_kernels() -> list:

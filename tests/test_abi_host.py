@@ -114,6 +114,9 @@ def test_device_entry_points_fail_loudly_without_gpu():
     assert R.last_kernels() == []  # nothing launched by the failed call
     with pytest.raises(R.NotEnoughShards):  # validation first
         R.reconstruct_warm(10, 4, 4096, [0] * 5 + [1] * 9)
+    R.debug_fail_alloc(-1)  # injection arms / disarms without a device
+    assert R.debug_fail_alloc(-1) == 0
+    assert R.debug_release_caches() == 0
 
 
 def test_kernel_selection_network(monkeypatch):

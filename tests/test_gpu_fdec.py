@@ -57,6 +57,29 @@ def test_fdec_random_patterns(oracle, fdec, k, m):
         assert (got == data[:, present[:k] == 0]).all(), (k, m, sorted(lost))
 
 
+@pytest.mark.parametrize("k,m", FDEC_KM)
+def test_pdec_pattern_compiled(oracle, monkeypatch, k, m):
+    """The fused reconstruct with the pattern compiled in (fftnet::Spec::present: constant
+    locator multiplies, static rows / blocks / outputs, pruned butterflies), reached through
+    rs_reconstruct_warm; random losses incl. surplus recovery rows, against the data."""
+    monkeypatch.delenv("RS_AMD_FDEC", raising=False)
+    rng = np.random.default_rng(k * 7907 + m)
+    sb, n = 4096, 3
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = oracle.encode_batch(k, m, data, threads=4)
+    for trial in range(2):
+        e = int(rng.integers(max(1, min(k, m) // 2), min(k, m) + 1)) if trial else min(k, m)
+        lost = list(rng.choice(k, size=e, replace=False))
+        lost += [k + int(i) for i in rng.choice(m, size=int(rng.integers(0, m - e + 1)), replace=False)]
+        present = np.ones(k + m, np.uint8)
+        present[lost] = 0
+        R.reconstruct_warm(k, m, sb, present)
+        got = reconstruct(k, m, present, data, par)
+        ran = R.last_kernels()
+        assert (got == data[:, present[:k] == 0]).all(), (k, m, sorted(lost), ran)
+        assert any(x.startswith(("rs_fft_pdecode", "rs_net_reconstruct", "rs_fft_inverse")) for x in ran), ran
+
+
 def test_fdec_vs_oracle_reconstruct(oracle, fdec):
     k, m, sb, n = 100, 20, 2048, 2
     rng = np.random.default_rng(100020)

@@ -1,9 +1,11 @@
 """Which kernel a reconstruct actually launches (rs_last_kernels) and the warm-up recipes of
 include/reedsol.h / INTEGRATION.md: a wide-code pattern's first calls run the fused FFT
-reconstruct (the pattern as data); where the pattern's e x e syndrome network beats it, two
-calls + rs_net_wait, or one rs_reconstruct_warm, bring the pattern to that network, and the
-next call launches it. Restored shards are checked against the data every time (MDS:
-restored originals are unique). Reference: root.zig:268-335 (Decoder.decode)."""
+reconstruct with the pattern as data (rs_fft_decode_*); its second call queues the same
+kernel with the pattern compiled in (rs_fft_pdecode_*), and two calls + rs_net_wait, or one
+rs_reconstruct_warm, bring the pattern to it: the next call launches it. RS_AMD_FDEC=0 keeps
+the round-2 form (syndromes + the pattern's e x e network), RS_AMD_FDEC=1 the pattern as
+data. Restored shards are checked against the data every time (MDS: restored originals are
+unique). Reference: root.zig:268-335 (Decoder.decode)."""
 import numpy as np
 import pytest
 
@@ -69,24 +71,33 @@ def test_first_call_runs_fused(c4_batch, monkeypatch):
     assert has(ran, "rs_fft_decode_k200_m55"), ran
 
 
-def test_warm_reaches_network(c4_batch, monkeypatch):
-    """rs_reconstruct_warm: the next call launches the pattern's 55 x 55 syndrome network."""
+def test_warm_reaches_pattern_kernel(c4_batch, monkeypatch):
+    """rs_reconstruct_warm: the next call launches the pattern-compiled fused kernel."""
     monkeypatch.delenv("RS_AMD_FDEC", raising=False)
     lost, present = pattern(402)
     R.reconstruct_warm(K, M, SB, present)
     ran = run(present, lost, c4_batch)
-    assert has(ran, "rs_net_syndrome_i55_o55"), ran
+    assert has(ran, "rs_fft_pdecode_k200_m55"), ran
     assert not has(ran, "rs_fft_decode"), ran
 
 
-def test_two_calls_and_net_wait_reach_network(c4_batch, monkeypatch):
+def test_two_calls_and_net_wait_reach_pattern_kernel(c4_batch, monkeypatch):
     """The INTEGRATION.md recipe without the warm call: two calls, rs_net_wait, then the
-    network (the upgrade job queues the compile behind the plan build)."""
+    pattern-compiled kernel (the upgrade job queues its compile behind the plan build)."""
     monkeypatch.delenv("RS_AMD_FDEC", raising=False)
     lost, present = pattern(403)
     assert has(run(present, lost, c4_batch), "rs_fft_decode")
     run(present, lost, c4_batch)
     R.net_wait()
+    ran = run(present, lost, c4_batch)
+    assert has(ran, "rs_fft_pdecode_k200_m55"), ran
+
+
+def test_warm_network_form(c4_batch, monkeypatch):
+    """RS_AMD_FDEC=0: the round-2 steady state, syndromes + the pattern's 55 x 55 network."""
+    monkeypatch.setenv("RS_AMD_FDEC", "0")
+    lost, present = pattern(406)
+    R.reconstruct_warm(K, M, SB, present)
     ran = run(present, lost, c4_batch)
     assert has(ran, "rs_net_syndrome_i55_o55"), ran
 
@@ -99,10 +110,12 @@ def test_forced_fused_after_warm(c4_batch, monkeypatch):
     assert has(ran, "rs_fft_decode_k200_m55") and not has(ran, "rs_net_syndrome"), ran
 
 
-def test_few_losses_stay_fused_or_direct(c4_batch, monkeypatch):
-    """20 losses: the fused kernel is the steady state (no network beats it)."""
+@pytest.mark.parametrize("e", [1, 8, 20, 40])
+def test_pattern_kernel_loss_counts(c4_batch, monkeypatch, e):
+    """Any loss count: after the warm-up the pattern-compiled kernel (or, for few losses, the
+    pattern's direct network) restores the data."""
     monkeypatch.delenv("RS_AMD_FDEC", raising=False)
-    lost, present = pattern(405, e=20)
+    lost, present = pattern(405 + e, e=e)
     R.reconstruct_warm(K, M, SB, present)
     ran = run(present, lost, c4_batch)
-    assert has(ran, "rs_fft_decode_k200_m55"), ran
+    assert has(ran, "rs_fft_pdecode_k200_m55") or has(ran, "rs_net_reconstruct_i200"), ran
