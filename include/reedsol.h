@@ -175,21 +175,27 @@ int rs_reconstruct_batch_host_multi(uint64_t original_count, uint64_t recovery_c
                                     uint64_t restored_stripe_stride, uint32_t flags, const int *devices,
                                     int n_devices);
 
-/* Which device kernel a call would run on ("net_encode_i10_o4", "encode_reg_w4_nv4",
- * "decode_matrix_e4_nv4", "encode_generic_nv1", "net_fft_encode_i200_o55", ...), assuming
- * 16-byte aligned buffers. present: k+m flags as for rs_reconstruct_batch_dev, or NULL for
- * "the first min(k, m) originals lost". net_<role>_* = bit-sliced XOR network (or
- * bit-sliced FFT kernel, net_fft_*) generated for the plan and compiled with hipRTC on
- * first use (shards of 1 / 2 KiB or whole 4 KiB units, <= 64 outputs; up to 64 input blocks
- * compile in the call, larger maps in the background; disable with RS_AMD_JIT=0). */
+/* Which device kernel a call would run on in its steady state ("net_encode_i10_o4",
+ * "encode_reg_w4_nv4", "decode_matrix_e4_nv4", "encode_generic_nv1",
+ * "net_fft_encode_i200_o55", "net_fft_pdecode_i200_o55", ...), assuming 16-byte aligned
+ * buffers. present: k+m flags as for rs_reconstruct_batch_dev, or NULL for "the first
+ * min(k, m) originals lost". net_<role>_* = bit-sliced XOR network (or bit-sliced FFT
+ * kernel, net_fft_*) generated for the plan and compiled with hipRTC on first use (shards of
+ * 1 / 2 KiB or whole 4 KiB units, <= 64 outputs; up to 64 input blocks compile in the call,
+ * larger maps in the background; disable with RS_AMD_JIT=0). A prediction: the kernels a
+ * call actually launched are in rs_last_kernels. */
 const char *rs_encode_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes);
 const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                        const uint8_t *present);
 /* Path rs_reconstruct_batch_dev_patterns takes for these arguments (16-byte aligned
- * buffers): "psyn_k<k>_m<m>" (the code's syndrome network + per-stripe solve),
- * "fft_syndromes+psyn_solve" (wide codes, chunk 32 / 64, any max_e: FFT kernel with
- * per-stripe masks + the e x e solve in output groups of 8),
- * "pattern_matrix" (per-stripe e x k table matrices) or "pattern_fft" (FFT kernels). */
+ * buffers): "psyn_k<k>_m<m>" (k <= 256, m <= 8, whole 4 KiB units: the code's syndrome
+ * network + a per-stripe solve), "fft_decode" (chunk 16 / 32 / 64 codes with max_e >= 0.6 m,
+ * or shards of whole 2 KiB units: the fused FFT reconstruct with per-stripe decode blocks
+ * built on the GPU), "fft_syndromes+psyn_solve" (chunk 16 / 32 / 64 otherwise: FFT syndromes
+ * with per-stripe masks + the e x e solve in output groups of 8), "pattern_matrix"
+ * (per-stripe e x k table matrices, W <= 32, max_e <= 8) or "pattern_fft" (the reference's
+ * decode on the generic FFT kernels: D1, D2-dropping codes, everything else). These are
+ * what a call is planned to run; rs_last_kernels reports what it did run. */
 const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                     uint32_t max_e, uint32_t flags);
 
@@ -232,6 +238,10 @@ int64_t rs_debug_fail_alloc(int64_t n);
  * pooled one-shot contexts; compiled kernels stay loaded), after any background plan build
  * finished. *pooled_contexts (optional) = one-shot contexts left in the pool (0). */
 int rs_debug_release_caches(uint64_t *pooled_contexts);
+/* Measurement builds of the FFT kernels (RS_AMD_FFT_DEBUG bit 6, rs_fftnet.cpp): every wave
+ * of workgroup 0 stamps s_memtime around each barrier of its third unit; copies the current
+ * device's 8 x 64 stamps (wave-major) to out[0, min(n, 512)). */
+int rs_debug_fft_stamps(uint64_t *out, uint64_t n);
 
 /* hipRTC activity of this process: kernels compiled, code objects found in the on-disk
  * cache ($RS_AMD_CACHE_DIR, else $XDG_CACHE_HOME/rs_amd or ~/.cache/rs_amd; empty = off),
@@ -247,8 +257,8 @@ int rs_net_compile_check(uint64_t original_count, uint64_t recovery_count, const
 
 /* Generate the per-stripe syndrome-network reconstruct kernels of
  * rs_reconstruct_batch_dev_patterns (rs_psyn.hpp) and compile them with hipRTC (no
- * device): for k <= 64, m <= 4 the code's fixed k -> m syndrome network plus the
- * per-stripe e x e solve; for wide codes (chunk 32 / 64) the FFT syndrome kernel with
+ * device): for k <= 256, m <= 8 the code's fixed k -> m syndrome network plus the
+ * per-stripe e x e solve; for chunk 16 / 32 / 64 codes the FFT syndrome kernel with
  * per-stripe masks plus the generic solve. RS_ERR_INVALID_ARGUMENT if the code has none. */
 int rs_psyn_compile_check(uint64_t original_count, uint64_t recovery_count, uint32_t flags, double *compile_ms,
                           uint64_t *code_bytes);

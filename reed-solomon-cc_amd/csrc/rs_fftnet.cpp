@@ -228,18 +228,24 @@ typedef unsigned long long u64;
 typedef u32 v4 __attribute__((ext_vector_type(4)));
 #define X3(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
 #define MUX(a, b, m) __builtin_amdgcn_bitop3_b32((a), (b), (m), 0xE4)
-#define XM(d, n) __builtin_amdgcn_bitop3_b32((d), (n), 0x0F0F0F0Fu, 0x78)
-#define SWN(a) MUX((a) >> 4, (a) << 4, 0x0F0F0F0Fu)
+// the nibble / bit-pair / bit masks: in VGPRs when RS_VMASK (a VALU instruction that
+// reads an SGPR issues at ~2/3 rate when two waves share the SIMD: 3.67 vs 2.67 cycles per
+// v_bitop3, profiles/r04/valu_probe2.log), else literals the compiler keeps in SGPRs
+struct Km {
+  u32 f, t, s;
+};
+#define XM(d, n) __builtin_amdgcn_bitop3_b32((d), (n), KM.f, 0x78)
+#define SWN(a) MUX((a) >> 4, (a) << 4, KM.f)
 #define TRS(j, d, m)                 \
   {                                  \
     const u32 a = x[j], b = x[j + d]; \
     x[j] = MUX(a, b << d, m);        \
     x[j + d] = MUX(a >> d, b, m);    \
   }
-__device__ __forceinline__ void tr8(u32 *x) {
-  TRS(0, 4, 0x0F0F0F0Fu) TRS(1, 4, 0x0F0F0F0Fu) TRS(2, 4, 0x0F0F0F0Fu) TRS(3, 4, 0x0F0F0F0Fu)
-  TRS(0, 2, 0x33333333u) TRS(1, 2, 0x33333333u) TRS(4, 2, 0x33333333u) TRS(5, 2, 0x33333333u)
-  TRS(0, 1, 0x55555555u) TRS(2, 1, 0x55555555u) TRS(4, 1, 0x55555555u) TRS(6, 1, 0x55555555u)
+__device__ __forceinline__ void tr8(u32 *x, const Km KM) {
+  TRS(0, 4, KM.f) TRS(1, 4, KM.f) TRS(2, 4, KM.f) TRS(3, 4, KM.f)
+  TRS(0, 2, KM.t) TRS(1, 2, KM.t) TRS(4, 2, KM.t) TRS(5, 2, KM.t)
+  TRS(0, 1, KM.s) TRS(2, 1, KM.s) TRS(4, 1, KM.s) TRS(6, 1, KM.s)
 }
 // raw buffer accesses: voffset = the lane's offset in the unit, soffset = the
 // (wave-uniform) shard offset; a resource with 0 records reads zeros
@@ -258,17 +264,17 @@ __device__ __forceinline__ void tr8(u32 *x) {
 // 2 KiB slice of a shard: lanes 0-31 read the lo halves, 32-63 the hi halves of
 // 16 chunks per KiB; one v_permlane32_swap per dword pairs them; then an 8x8 bit
 // transpose per byte lane: P[j] = (lo plane j | hi plane j) per byte (nibbles)
-__device__ __forceinline__ void planes2(v4 a, v4 b, u32 *P) {
+__device__ __forceinline__ void planes2(v4 a, v4 b, u32 *P, const Km KM) {
 #pragma unroll
   for (int v = 0; v < 4; v++) {
     const auto s = __builtin_amdgcn_permlane32_swap(a[v], b[v], false, false);
     P[v] = s[0];
     P[4 + v] = s[1];
   }
-  tr8(P);
+  tr8(P, KM);
 }
-__device__ __forceinline__ void unplanes2(u32 *P, v4 &a, v4 &b) {
-  tr8(P);
+__device__ __forceinline__ void unplanes2(u32 *P, v4 &a, v4 &b, const Km KM) {
+  tr8(P, KM);
 #pragma unroll
   for (int v = 0; v < 4; v++) {
     const auto s = __builtin_amdgcn_permlane32_swap(P[v], P[4 + v], false, false);
@@ -289,6 +295,14 @@ __device__ __forceinline__ void unplanes2(u32 *P, v4 &a, v4 &b) {
     __builtin_amdgcn_s_barrier();                                  \
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); \
   }
+// RS_AMD_FFT_DEBUG bit 6 (measurement builds): lane 0 of every wave of workgroup 0 stamps
+// s_memtime around each barrier of its third unit into stamps[w * 64 + i]
+#define STAMP(i)                                                         \
+  if (RS_STAMPS && stamp_on && lane == 0u) {                             \
+    asm volatile("" ::: "memory");                                       \
+    stamps[w * 64u + (i)] = __builtin_amdgcn_s_memtime();                \
+    asm volatile("" ::: "memory");                                       \
+  }
 // Spec::decode: multiplication by a uniform runtime scalar from its 128 nibble masks
 // (scalar_masks), read through the constant address space (scalar loads):
 // out_i = XOR_j (x_j & M[16 i + j]) ^ (SWN(x_j) & M[16 i + 8 + j])
@@ -298,7 +312,7 @@ typedef const __attribute__((address_space(4))) u32 *cptr;
 #ifndef RS_RMUL_G
 #define RS_RMUL_G 1
 #endif
-__device__ __forceinline__ void rmul(u32 *x, cptr M) {
+__device__ __forceinline__ void rmul(u32 *x, cptr M, const Km KM) {
 #ifdef RS_DBG_NORMUL
   return;
 #endif
@@ -360,6 +374,22 @@ int prefetch_of(const Spec &s) {
 // decode kernels stop after Enc(d') (no decode tail), bit 3 decode: no runtime multiplies,
 // bit 4 decode: the round-3 load order (rec rows loaded at the tail, no prefetch)
 int debug_of() { return env_int("RS_AMD_FFT_DEBUG", 0); }
+
+// the stamp buffer of measurement builds (8 waves x 64 u64 per device)
+std::mutex g_stamp_mu;
+std::map<int, unsigned long long *> g_stamp_bufs;
+unsigned long long *stamp_buffer(int dev) {
+  std::lock_guard<std::mutex> lk(g_stamp_mu);
+  unsigned long long *&p = g_stamp_bufs[dev];
+  if (!p && hipMalloc(reinterpret_cast<void **>(&p), 8 * 64 * 8) == hipSuccess) (void)hipMemset(p, 0, 8 * 64 * 8);
+  return p;
+}
+
+// the transpose / basis masks in VGPRs (RS_AMD_FFT_VMASK, default on)
+int vmask_of() { return env_int("RS_AMD_FFT_VMASK", 1) ? 1 : 0; }
+
+// s_setprio alternation between the SIMD-pair halves every n butterflies (0: off)
+int prio_of() { return std::max(0, env_int("RS_AMD_FFT_PRIO", 0)); }
 
 // runtime-multiply masks through vector loads (RS_AMD_FFT_RMULV=1) instead of scalar loads
 int rmul_vload() { return env_int("RS_AMD_FFT_RMULV", 0) ? 1 : 0; }
@@ -489,9 +519,9 @@ struct Gen {
     rows(ins, rm, tl, false);
     for (int i = 0; i < 8; i++) {
       if (acc)
-        o << "  " << dst[i] << " ^= MUX(" << tl[i] << ", " << tl[8 + i] << ", 0x0F0F0F0Fu);\n";
+        o << "  " << dst[i] << " ^= MUX(" << tl[i] << ", " << tl[8 + i] << ", KM.f);\n";
       else
-        o << "  " << dst[i] << " = MUX(" << tl[i] << ", " << tl[8 + i] << ", 0x0F0F0F0Fu);\n";
+        o << "  " << dst[i] << " = MUX(" << tl[i] << ", " << tl[8 + i] << ", KM.f);\n";
       op(acc ? 2 : 1);
     }
   }
@@ -513,12 +543,22 @@ struct Gen {
 
   int sched = 0;  // sched_barrier every `sched` butterflies (bounds the scheduler's interleaving)
   int nbf = 0;
+  // SIMD-pair arbitration (RS_AMD_FFT_PRIO = n): waves w and w + 4 share a SIMD and the
+  // younger loses VALU arbitration to the older (MI355X_MICROARCH.md, two waves per SIMD),
+  // so in a phase of equal work it finishes last and every barrier waits for it. Every n
+  // butterflies the two halves swap s_setprio, so they take turns.
+  int prio = 0, nprio = 0, pturn = 0;
 
   // one butterfly on named 8-dword positions with zero tracking
   void butterfly(const std::string &xn, bool &zx, const std::string &yn, bool &zy, bool inv, const Tw &t) {
     const auto X = regs(xn), Y = regs(yn);
     if (zx && zy) return;
     if (sched && ++nbf % sched == 0) o << "  __builtin_amdgcn_sched_barrier(0);\n";
+    if (prio && ++nprio % prio == 0) {
+      pturn ^= 1;
+      o << "  if (w & 4u) __builtin_amdgcn_s_setprio(" << pturn << "); else __builtin_amdgcn_s_setprio(" << (pturn ^ 1)
+        << ");\n";
+    }
     if (t.zero && st) st->xor_only++;
     if (inv) {  // ifftPartial, Generic.zig:171-192: y ^= x; x ^= M y
       if (!zx) {
@@ -598,6 +638,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   Gen g;
   g.st = stats;
   g.sched = sched_of();  // sched_barrier per butterfly: bounds the scheduler's interleaving (compile time)
+  g.prio = prio_of();
   Stats dummy;
   if (!g.st) g.st = &dummy;
   std::ostringstream &o = g.o;
@@ -642,7 +683,8 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         cg_log[g] = c ? T.log[c] : kModulus + 1u;
       }
   }
-  o << "#define RS_AUX_LD 2\n#define RS_AUX_ST 2\n" << (s.decode && (dbg & 8) ? "#define RS_DBG_NORMUL 1\n" : "")
+  o << "#define RS_AUX_LD 2\n#define RS_AUX_ST 2\n#define RS_STAMPS " << ((dbg & 64) ? 1 : 0) << "\n"
+    << (s.decode && (dbg & 8) ? "#define RS_DBG_NORMUL 1\n" : "")
     << "#define RS_RMUL_G " << rmul_group() << "\n" << (rmul_vload() ? "#define RS_RMUL_VLOAD 1\n" : "") << kPrelude;
   // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
@@ -673,9 +715,11 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   o << "extern \"C\" __global__ __launch_bounds__(" << NW * 64 << ") void " << name
     << "(const unsigned char *__restrict__ data, u64 ds, const unsigned char *__restrict__ rec, u64 rs,\n"
        "    unsigned char *__restrict__ out, u64 os, u32 sb, u32 ups, u64 n_units, u64 n_st,\n"
-       "    const u32 *__restrict__ dm, u32 dmw) {\n"
+       "    const u32 *__restrict__ dm, u32 dmw, u64 *__restrict__ stamps) {\n"
     << "  __shared__ u32 xch[" << C * 8 * 64 << "];\n"
     << "  v4 *const xch4 = (v4 *)xch;\n"
+    << "  Km KM = {0x0F0F0F0Fu, 0x33333333u, 0x55555555u};\n"
+    << (vmask_of() ? "  asm volatile(\"\" : \"+v\"(KM.f), \"+v\"(KM.t), \"+v\"(KM.s));\n" : "")
     << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
        "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
        "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
@@ -704,6 +748,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   std::ostringstream hdr2;
   hdr2 << "#pragma unroll 1\n"
     << "  for (u64 u = ub; u < ue; u += step) {\n"
+    << "  const bool stamp_on = blockIdx.x == 0u && u == ub + 2u * step;\n  STAMP(62u);\n"
     << 
        "  u32 sbl = sb;\n"
        "  asm volatile(\"\" : \"+s\"(sbl));  // shard offsets are recomputed per unit (SALU), not hoisted into VGPRs\n"
@@ -733,6 +778,12 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     o << "  }\n";
   };
 
+  int nstamp = 0;  // STAMP ids (measurement builds)
+  auto bar = [&]() {
+    const std::string a = std::to_string(std::min(nstamp, 61)), b = std::to_string(std::min(nstamp + 1, 61));
+    nstamp += 2;
+    return "  STAMP(" + a + "u); BAR(); STAMP(" + b + "u);\n";
+  };
   // ---- loads of chunk j (layout A: wave w reads positions w*8 + r), raw into la/lb
   std::vector<uint8_t> declared(P.truncs.size(), 0);
   auto emit_loads = [&](size_t j, uint32_t r0, uint32_t r1, const char *rd = "RD", const char *uo0 = "uo",
@@ -788,7 +839,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       bool any = false;
       for (uint32_t w = 0; w < NW; w++) any |= (vm[w] >> r & 1) != 0;
       if (!any) continue;
-      o << "  { u32 Q[8]; planes2(la" << j << "[" << r << "], lb" << j << "[" << r << "], Q);\n";
+      o << "  { u32 Q[8]; planes2(la" << j << "[" << r << "], lb" << j << "[" << r << "], Q, KM);\n";
       for (int i = 0; i < 8; i++) o << "  w" << r << "_" << i << " = Q[" << i << "];\n";
       g.op(4 + 48);
       const auto W = Gen::regs(wname(r));
@@ -839,14 +890,14 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       }
       o << "  }\n";
     }
-    o << "  BAR();\n";
+    o << bar();
     bool zb[8];
     for (uint32_t t = 0; t < 8; t++) {
       zb[t] = !liveB[t];
       if (!liveB[t]) continue;
       lds_read("(w * 8u)", t, Gen::regs(bname(t)));
     }
-    o << "  BAR();\n  }\n";  // every wave has read its slots: the next exchange may write
+    o << bar() << "  }\n";  // every wave has read its slots: the next exchange may write
     // ---- layout B layers (bits >= 3), one code path for all waves
     g.ops = &g.st->ops_b;
     for (const Layer &L : P.ifft[j]) {
@@ -950,12 +1001,12 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     if (!needB[t] || zc[t]) continue;
     lds_write("w", t << P.WB, Gen::regs(cname(t)));
   }
-  o << "  BAR();\n";
+  o << bar();
   for (uint32_t r = 0; r < 8; r++) {
     if (!readA[r]) continue;
     lds_read("(w * 8u)", r, Gen::regs(wname(r)));
   }
-  o << "  BAR();\n  }\n";
+  o << bar() << "  }\n";
   g.ops = &g.st->ops_a;
   bool first = true;
   for (uint32_t w = 0; w < NW; w++) {
@@ -998,7 +1049,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         g.basis_change(W);
       o << "  { u32 Q[8] = {";
       for (int i = 0; i < 8; i++) o << W[i] << (i < 7 ? ", " : "};\n");
-      o << "    v4 a, b; unplanes2(Q, a, b);\n";
+      o << "    v4 a, b; unplanes2(Q, a, b, KM);\n";
       g.op(4 + 48);
       o << "    const u32 so = " << p << "u * sbl;\n";
       if (P.out_mode[p] == kOutXorRec) o << "    a ^= LDB(RR, uo, so); b ^= LDB(RR1, uo1, so);\n";
@@ -1062,7 +1113,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         const uint32_t p = P.posA(w, r);
         const auto W = Gen::regs(wname(r));
         g.ops = &g.st->ops_io;
-        o << "  __builtin_amdgcn_sched_barrier(0);\n  { u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q);\n";
+        o << "  __builtin_amdgcn_sched_barrier(0);\n  { u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q, KM);\n";
         std::vector<std::string> q(8);
         for (int i = 0; i < 8; i++) q[i] = "Q[" + std::to_string(i) + "]";
         g.basis_change(q);
@@ -1088,13 +1139,13 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       }
       o << "  }\n";
     }
-    o << "  BAR();\n";
+    o << bar();
     bool za[8];
     for (uint32_t t = 0; t < 8; t++) {
       za[t] = !liveB[t];
       if (liveB[t]) lds_read("(w * 8u)", t, Gen::regs(cname(t)));
     }
-    o << "  BAR();\n  }\n";
+    o << bar() << "  }\n";
     g.ops = &g.st->ops_b;
     for (const Layer &L : il) {
       if (P.inA(L.bit)) continue;
@@ -1174,10 +1225,10 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       o << "  {\n  LQ();\n";
       for (uint32_t t = 0; t < 8; t++)
         if (nB[t] && !zb[t]) lds_write("w", t << P.WB, Gen::regs(bn(t)));
-      o << "  BAR();\n";
+      o << bar();
       for (uint32_t r = 0; r < 8; r++)
         if (rA[r]) lds_read("(w * 8u)", r, Gen::regs(wname(r)));
-      o << "  BAR();\n  }\n";
+      o << bar() << "  }\n";
       // A layers and the erased shards' outputs, per wave
       bool firstw = true;
       for (uint32_t w = 0; w < NW; w++) {
@@ -1214,7 +1265,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
           }
           o << "  __builtin_amdgcn_sched_barrier(0);\n  { u32 X[8] = {";
           for (int i = 0; i < 8; i++) o << W[i] << (i < 7 ? ", " : "};\n");
-          o << "  v4 a, b; unplanes2(X, a, b);\n  STB(a, RO, uo, " << out_row[gi] << "u * sbl); STB(b, RO1, uo1, "
+          o << "  v4 a, b; unplanes2(X, a, b, KM);\n  STB(a, RO, uo, " << out_row[gi] << "u * sbl); STB(b, RO1, uo1, "
             << out_row[gi] << "u * sbl); }\n";
         }
         o << "  }\n";
@@ -1231,13 +1282,13 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     if (old_order) emit_rec_loads();
     for (uint32_t r = 0; r < 8; r++) {
       const auto W = Gen::regs(wname(r));
-      o << "  if (us" << r << ") {\n  u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q);\n";
+      o << "  if (us" << r << ") {\n  u32 Q[8]; planes2(ra" << r << ", rb" << r << ", Q, KM);\n";
       std::vector<std::string> q(8);
       for (int i = 0; i < 8; i++) q[i] = "Q[" + std::to_string(i) + "]";
       g.basis_change(q);
       o << "  u32 X[8] = {";
       for (int i = 0; i < 8; i++) o << W[i] << " ^ Q[" << i << "]" << (i < 7 ? ", " : "};\n");
-      o << "  rmul(X, (cptr)(DM + " << mko << "u + pd" << r << " * 128u));\n";
+      o << "  rmul(X, (cptr)(DM + " << mko << "u + pd" << r << " * 128u), KM);\n";
       for (int i = 0; i < 8; i++) o << "  " << W[i] << " = X[" << i << "];\n";
       o << "  } else {\n";
       for (int i = 0; i < 8; i++) o << "  " << W[i] << " = 0u;\n";
@@ -1284,13 +1335,13 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       }
       o << "  }\n";
     }
-    o << "  BAR();\n";
+    o << bar();
     bool za[8];
     for (uint32_t t = 0; t < 8; t++) {
       za[t] = !liveB[t];
       if (liveB[t]) lds_read("(w * 8u)", t, Gen::regs(cname(t)));
     }
-    o << "  BAR();\n  }\n";
+    o << bar() << "  }\n";
     g.ops = &g.st->ops_b;
     for (const Layer &L : il) {
       if (P.inA(L.bit)) continue;
@@ -1344,10 +1395,10 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       o << "  {\n  LQ();\n";
       for (uint32_t t = 0; t < 8; t++)
         if (nB[t] && !zb[t]) lds_write("w", t << P.WB, Gen::regs(bn(t)));
-      o << "  BAR();\n";
+      o << bar();
       for (uint32_t r = 0; r < 8; r++)
         if (rA[r]) lds_read("(w * 8u)", r, Gen::regs(wname(r)));
-      o << "  BAR();\n  }\n";
+      o << bar() << "  }\n";
       g.ops = &g.st->ops_a;
       bool firstw = true;
       for (uint32_t w = 0; w < NW; w++) {
@@ -1384,17 +1435,17 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         o << "  { const u32 q = w * 8u + " << r << "u;\n  const u32 row = q < " << tK << "u ? DMc[" << dwm + 3 + g0
           << "u + q] : 0xFFFFFFFFu;\n  if (row != 0xFFFFFFFFu) {\n  u32 X[8] = {";
         for (int i = 0; i < 8; i++) o << W[i] << (i < 7 ? ", " : "};\n");
-        o << "  rmul(X, (cptr)(DM + " << mko + 128 * (s.m + g0) << "u + q * 128u));\n";
+        o << "  rmul(X, (cptr)(DM + " << mko + 128 * (s.m + g0) << "u + q * 128u), KM);\n";
         std::vector<std::string> xs(8);
         for (int i = 0; i < 8; i++) xs[i] = "X[" + std::to_string(i) + "]";
         g.basis_change(xs);
-        o << "  v4 a, b; unplanes2(X, a, b);\n  const u32 so = row * sbl;\n  STB(a, RO, uo, so); STB(b, RO1, uo1, so);\n"
+        o << "  v4 a, b; unplanes2(X, a, b, KM);\n  const u32 so = row * sbl;\n  STB(a, RO, uo, so); STB(b, RO1, uo1, so);\n"
           << "  }\n  }\n";
       }
       o << "  }\n";
     }
   }
-  o << "  stripe = stripe_n; uu = uu_n;\n";
+  o << "  STAMP(63u);\n  stripe = stripe_n; uu = uu_n;\n";
   o << "  }\n}\n";
   return o.str();
 }
@@ -1426,7 +1477,8 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft4:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":d" +
-                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":v" + std::to_string(rmul_vload()) + ":" +
+                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":v" + std::to_string(rmul_vload()) +
+                  ":r" + std::to_string(prio_of()) + ":k" + std::to_string(vmask_of()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
@@ -1641,9 +1693,18 @@ hipError_t launch(const jit::Kernel &kn, const Spec &s, const uint8_t *data, uin
   unsigned char *o = out;
   const uint32_t *dm = dmask;
   uint32_t dmw = shared_mask ? 0u : dmask_words;  // the kernel's per-stripe mask stride
-  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st, &dm, &dmw};
+  unsigned long long *stamps = debug_of() & 64 ? stamp_buffer(dev) : nullptr;
+  void *args[] = {&d, &ds, &r, &rs, &o, &os, &sb32, &ups, &n_units, &n_st, &dm, &dmw, &stamps};
   trace_launch(kn.name.c_str());
   return hipModuleLaunchKernel(kn.fn, static_cast<uint32_t>(grid), 1, 1, (C / 8) * 64, 1, 1, 0, st, args, nullptr);
+}
+
+int read_stamps(uint64_t *host, size_t n) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  unsigned long long *p = stamp_buffer(dev);
+  if (!p || hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpy(host, p, std::min<size_t>(n, 8 * 64) * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
 uint64_t selftest(const Spec &s, int trials) {

@@ -131,6 +131,9 @@ uint64_t decode_selftest(uint32_t k, uint32_t m, uint32_t e, int trials);
 // T-coordinate matrices on scalar symbols and compares with scalar_encode.
 // Returns the number of mismatching symbols over `trials` random inputs.
 uint64_t selftest(const Spec &s, int trials);
+// measurement builds (RS_AMD_FFT_DEBUG bit 6): copy the phase stamps (8 waves x 64 s_memtime
+// values of workgroup 0's third unit) of the current device to host; 0 on success
+int read_stamps(uint64_t *host, size_t n);
 
 // Instruction estimate of the generated network ops (wave instructions per unit)
 struct Stats {

@@ -235,6 +235,11 @@ int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out
 int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft);
 
 constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
+// the low-rate generic kernels' cap: kScratchCap, or RS_AMD_SCRATCH_CAP_MB (tests)
+inline uint64_t scratch_cap() {
+  const char *e = std::getenv("RS_AMD_SCRATCH_CAP_MB");
+  return e && *e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20 : kScratchCap;
+}
 
 // ------------------------------------------------- kernel selection (rs_select.cpp)
 bool encode_net_async(uint64_t k, uint64_t m);

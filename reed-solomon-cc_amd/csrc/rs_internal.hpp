@@ -42,6 +42,9 @@ struct EncodeArgs {
   uint64_t scratch_stripes;
   bool contig;           // lane layout (dev::load_sym): contiguous waves vs split halves
   const uint32_t *skip = nullptr;  // device bitmask of k bits: data shards read as zero (syndrome reconstruct)
+  // low-rate generic encode: scratch regions per stripe (coefficients + one per recovery
+  // chunk of a launch; 0 = 1 + n_chunks) and the first recovery chunk of the launch
+  uint32_t regions = 0, chunk0 = 0;
 };
 
 // Reconstruct: positions per root.zig:199-229 (recovery at [0,m), originals at

@@ -981,9 +981,9 @@ template <int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_low_coef(EncodeArgs a) {
   uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
-  const uint64_t sb = a.shard_bytes, C = a.chunk;
+  const uint64_t sb = a.shard_bytes, C = a.chunk, R = a.regions ? a.regions : 1 + a.n_chunks;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    uint8_t *work = a.scratch + s * (1 + a.n_chunks) * C * sb;
+    uint8_t *work = a.scratch + s * R * C * sb;
     const XformIO ic{a.data + s * a.data_stripe_stride, sb, a.k, work, sb, work, sb, C, false, false, off};
     xform_ph<NV, true>(ic, C, a.k, a.tabs);
   }
@@ -993,12 +993,13 @@ template <int NV>
 __global__ __launch_bounds__(kBlock) void k_encode_low_generic(EncodeArgs a) {
   uint32_t off;
   if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
-  const uint64_t sb = a.shard_bytes, C = a.chunk, TI = ifft_tab_count_d(C), j = blockIdx.z;
+  const uint64_t sb = a.shard_bytes, C = a.chunk, TI = ifft_tab_count_d(C), j = a.chunk0 + blockIdx.z;
+  const uint64_t R = a.regions ? a.regions : 1 + a.n_chunks;
   const uint64_t t = a.m - j * C < C ? a.m - j * C : C;
   for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    uint8_t *work = a.scratch + s * (1 + a.n_chunks) * C * sb;
+    uint8_t *work = a.scratch + s * R * C * sb;
     uint8_t *dst = a.parity + s * a.parity_stripe_stride;
-    const XformIO fc{work, sb, C, work + (1 + j) * C * sb, sb, dst + j * C * sb, sb, t, true, a.contig, off};
+    const XformIO fc{work, sb, C, work + (1 + blockIdx.z) * C * sb, sb, dst + j * C * sb, sb, t, true, a.contig, off};
     xform_ph<NV, false>(fc, C, t, a.tabs + TI + j * a.tabs_per_chunk);
   }
 }
@@ -1759,13 +1760,20 @@ KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv) {
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
   trace_launch(kc.name);
   if (kc.variant == Variant::kGeneric) {
-    // a.scratch: (1 + n_chunks) C positions per stripe (low_encode)
+    // a.scratch: `regions` C-position regions per stripe (low_encode): the coefficients, then
+    // one per recovery chunk of a launch; the chunks run in groups of regions - 1
     const dim3 g = grid_for(a.shard_bytes, 1, a.n_stripes);
     hipLaunchKernelGGL(k_encode_low_coef<1>, g, dim3(kBlock), 0, s, a);
     if (hipError_t e = hipGetLastError()) return e;
-    if (a.n_chunks > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_encode_low_generic<1>, dim3(g.x, g.y, static_cast<uint32_t>(a.n_chunks)), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
+    const uint32_t G = a.regions ? a.regions - 1 : a.n_chunks;
+    if (G == 0 || G > 65535) return hipErrorInvalidValue;
+    for (uint32_t j0 = 0; j0 < a.n_chunks; j0 += G) {
+      EncodeArgs b = a;
+      b.chunk0 = j0;
+      hipLaunchKernelGGL(k_encode_low_generic<1>, dim3(g.x, g.y, std::min(G, a.n_chunks - j0)), dim3(kBlock), 0, s, b);
+      if (hipError_t e = hipGetLastError()) return e;
+    }
+    return hipSuccess;
   }
   for (uint64_t s0 = 0; s0 < a.n_stripes; s0 += 65535) {
     EncodeArgs b = a;

@@ -227,7 +227,7 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
 // generic kernels walk a scratch of `per_stripe` positions x sb per stripe, in slices
 template <class F>
 int in_scratch_slices(uint64_t n, uint64_t per_stripe_bytes, hipStream_t s, F &&launch) {
-  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n, kScratchCap / per_stripe_bytes));
+  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n, scratch_cap() / per_stripe_bytes));
   void *scratch = nullptr;
   HIP_TRY(dev_malloc_async(&scratch, per * per_stripe_bytes, s));
   hipError_t e = hipSuccess;
@@ -268,8 +268,14 @@ int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const u
     HIP_TRY(launch_encode_low(kc, a, s));
     return RS_OK;
   }
-  // coefficients + one intermediate region per recovery chunk (the chunks' FFTs run in parallel)
-  return in_scratch_slices(n, (1ull + p->n_chunks) * p->C * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
+  // coefficients + one intermediate region per recovery chunk (the chunks' FFTs run in
+  // parallel), in groups of G chunks so that a stripe's (1 + G) regions fit the scratch cap
+  // (G = 1 at least: two regions per stripe)
+  const uint64_t region = static_cast<uint64_t>(p->C) * sb;
+  const uint64_t fit = scratch_cap() / region;  // regions of one stripe that fit the cap
+  const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(p->n_chunks, fit > 1 ? fit - 1 : 1));
+  a.regions = static_cast<uint32_t>(1 + G);
+  return in_scratch_slices(n, (1 + G) * region, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
     EncodeArgs b = a;
     b.data += s0 * ostride;
     b.parity += s0 * rstride;

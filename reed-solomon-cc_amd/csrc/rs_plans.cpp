@@ -600,6 +600,13 @@ int rs_fft_pdecode_compile_check(uint64_t k, uint64_t m, const uint8_t *present,
   });
 }
 
+int rs_debug_fft_stamps(uint64_t *out, uint64_t n) {
+  return guarded([&]() -> int {
+    if (!out) return fail(RS_ERR_INVALID_ARGUMENT, "out == NULL");
+    return fftnet::read_stamps(out, n) == 0 ? RS_OK : fail(RS_ERR_DEVICE, "stamp buffer unavailable");
+  });
+}
+
 int rs_fft_decode_selftest(uint64_t k, uint64_t m, uint32_t e, int trials, uint64_t *mismatches) {
   return guarded([&]() -> int {
     int st = check_codec(k, m, fftnet::kUnitBytes);

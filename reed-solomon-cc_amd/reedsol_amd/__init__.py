@@ -92,6 +92,7 @@ def lib():
         "rs_last_kernels": (C.c_char_p, []),
         "rs_debug_fail_alloc": (C.c_int64, [C.c_int64]),
         "rs_debug_release_caches": (C.c_int, [vp]),
+        "rs_debug_fft_stamps": (C.c_int, [vp, u64]),
         "rs_jit_stats": (C.c_int, [vp, vp, vp]),
         "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
         "rs_psyn_compile_check": (C.c_int, [u64, u64, u32, vp, vp]),
@@ -443,6 +444,14 @@ def debug_release_caches() -> int:
     n = C.c_uint64()
     _check(lib().rs_debug_release_caches(C.byref(n)))
     return n.value
+
+
+def debug_fft_stamps():
+    """Phase stamps of an FFT measurement build (RS_AMD_FFT_DEBUG bit 6): numpy uint64 [8, 64]."""
+    import numpy as np
+    a = np.zeros(8 * 64, np.uint64)
+    _check(lib().rs_debug_fft_stamps(a.ctypes.data_as(C.c_void_p), a.size))
+    return a.reshape(8, 64)
 
 
 def last_kernels() -> list:

@@ -136,14 +136,17 @@ def test_kernel_selection_network(monkeypatch):
     # wide codes (chunk 32 / 64): the bit-sliced FFT kernel (rs_fftnet.hpp)
     assert R.encode_kernel_name(200, 55, 1 << 18) == "net_fft_encode_i200_o55"
     assert R.encode_kernel_name(100, 20, 1 << 18) == "net_fft_encode_i100_o20"
-    # wide code, 55 erasures: the first calls run the fused FFT reconstruct (round 3), the
-    # steady state syndromes on the FFT kernel + the 55 x 55 map as a (background-compiled)
-    # network; 20 erasures: the fused kernel for good
-    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+net_fft_encode_i200_o55+net_syndrome_i55_o55"
+    # wide code, 55 / 20 erasures: the first calls run the fused FFT reconstruct with the
+    # pattern as data (round 3), the steady state the same kernel with the pattern compiled
+    # in (round 4, background-compiled); RS_AMD_FDEC=1 the pattern as data for good,
+    # RS_AMD_FDEC=0 syndromes on the FFT kernel + the 55 x 55 map as a network
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "net_fft_pdecode_i200_o55"
     p20 = [0] * 20 + [1] * 235
-    assert R.reconstruct_kernel_name(200, 55, 1 << 18, p20) == "net_fft_decode_i200_o55"
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18, p20) == "net_fft_pdecode_i200_o55"
     monkeypatch.setenv("RS_AMD_FDEC", "1")
     assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "net_fft_decode_i200_o55"
+    monkeypatch.setenv("RS_AMD_FDEC", "0")
+    assert R.reconstruct_kernel_name(200, 55, 1 << 18) == "syndrome+net_fft_encode_i200_o55+net_syndrome_i55_o55"
 
 
 def test_kernel_selection_async_cap(monkeypatch):

@@ -102,6 +102,7 @@ def test_syndrome_network_background_compile(oracle, monkeypatch):
     the calls after it the network — both restore the erased shards bit-exactly."""
     monkeypatch.delenv("RS_AMD_JIT", raising=False)
     monkeypatch.delenv("RS_AMD_JIT_SYNC", raising=False)
+    monkeypatch.setenv("RS_AMD_FDEC", "0")  # the syndrome path (round 2's steady state)
     k, m, sb, n = 200, 55, 8192, 2
     rng = np.random.default_rng(2055)
     data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)

@@ -248,3 +248,25 @@ def test_low_rate_widest_transforms(oracle, k, m):
     R.reconstruct_batch_dev(k, m, present, d, par, out)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), data)
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("cap_mb", ["1", "3", "64"])
+def test_low_rate_encode_scratch_cap(oracle, monkeypatch, cap_mb):
+    """The generic low-rate encode keeps a stripe's scratch within the cap: its recovery chunks
+    run in groups of G with (1 + G) C shard-regions per stripe (G = 1 when even two regions
+    exceed the cap). RS(300,1000) 4 KiB: C = 512, region 2 MiB, 2 chunks; cap 1 MiB (below
+    one stripe's two regions), 3 MiB (one chunk per launch), 64 MiB (both chunks at once)."""
+    monkeypatch.setenv("RS_AMD_SCRATCH_CAP_MB", cap_mb)
+    k, m, sb, n = 300, 1000, 4096, 3
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(300 + int(cap_mb))
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    par = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
+    R.encode_batch_dev(k, m, torch.from_numpy(data).to(dev), par)
+    torch.cuda.synchronize()
+    got = par.cpu().numpy()
+    for s in range(n):
+        st, exp = oracle.encode_low(k, m, data[s])
+        assert st == 0 and np.array_equal(got[s], exp), s

@@ -24,7 +24,9 @@ def main():
     axes = [(kv.split("=", 1)[0], kv.split("=", 1)[1].split(",")) for kv in sys.argv[6:]]
     variants = [tuple(zip([a[0] for a in axes], v)) for v in itertools.product(*[a[1] for a in axes])]
     rounds, reps = int(os.environ.get("ROUNDS", "4")), int(os.environ.get("REPS", "3"))
-    os.environ["RS_AMD_FDEC"] = "1"
+    form = os.environ.get("FORM", "dyn")  # dyn: the pattern as data; pattern: compiled in (warmed)
+    if form == "dyn":
+        os.environ["RS_AMD_FDEC"] = "1"
     dev = torch.device("cuda:0")
     lost = list(range(1, k, 3))[:e] if 3 * e <= k else list(range(e))
     present = [0 if i in lost else 1 for i in range(k)] + [1] * m
@@ -53,6 +55,8 @@ def main():
         for v in variants:
             for name, val in v:
                 os.environ[name] = val
+            if form == "pattern" and r == 0:
+                R.reconstruct_warm(k, m, sb, present)
             te = timed(lambda: R.encode_batch_dev(k, m, data, par, stream=s))
             ke = R.last_kernels()
             res[v]["ok_enc"] &= bool(torch.equal(par, ref))

@@ -11,10 +11,12 @@
 
 #define OPS8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
-enum Op { kPermVVV, kPermSVV, kBitop3, kXor, kXor3, kAnd, kMovS, kLshr, kAndOr, kBfe, kNumOps };
+enum Op { kPermVVV, kPermSVV, kBitop3, kXor, kXor3, kAnd, kMovS, kLshr, kAndOr, kBfe, kBitop3S, kBitop3Dep1,
+          kBitop3Dep2, kNumOps };
 static const char *kNames[] = {"v_perm_b32 v,v,v", "v_perm_b32 s,v,v", "v_bitop3_b32 v,v,v", "v_xor_b32",
                                "v_or3_b32",        "v_and_b32",        "v_mov_b32 v,s",      "v_lshrrev_b32",
-                               "v_and_or_b32",     "v_bfe_u32"};
+                               "v_and_or_b32",     "v_bfe_u32",        "v_bitop3_b32 v,v,s", "bitop3 1 chain",
+                               "bitop3 2 chains"};
 
 template <int OP>
 __global__ __launch_bounds__(256) void probe(uint32_t *out, uint64_t *cyc, uint32_t iters, uint32_t sval) {
@@ -37,7 +39,10 @@ __global__ __launch_bounds__(256) void probe(uint32_t *out, uint64_t *cyc, uint3
   if constexpr (OP == kMovS) asm volatile("v_mov_b32 %0, %1" : "=v"(x[c]) : "s"(sval + c));                \
   if constexpr (OP == kLshr) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(x[c]));                          \
   if constexpr (OP == kAndOr) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(x[c]) : "v"(a), "v"(sel)); \
-  if constexpr (OP == kBfe) asm volatile("v_bfe_u32 %0, %0, 3, 8" : "+v"(x[c]));
+  if constexpr (OP == kBfe) asm volatile("v_bfe_u32 %0, %0, 3, 8" : "+v"(x[c]));                           \
+  if constexpr (OP == kBitop3S) asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x96" : "+v"(x[c]) : "v"(a), "s"(sval)); \
+  if constexpr (OP == kBitop3Dep1) asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x96" : "+v"(x[0]) : "v"(a), "v"(sel)); \
+  if constexpr (OP == kBitop3Dep2) asm volatile("v_bitop3_b32 %0, %1, %0, %2 bitop3:0x96" : "+v"(x[c & 1]) : "v"(a), "v"(sel));
       OPS8(STEP)
 #undef STEP
     }
@@ -93,6 +98,9 @@ int main(int argc, char **argv) {
     run<kLshr>(blocks, iters, out, cyc);
     run<kAndOr>(blocks, iters, out, cyc);
     run<kBfe>(blocks, iters, out, cyc);
+    run<kBitop3S>(blocks, iters, out, cyc);
+    run<kBitop3Dep1>(blocks, iters, out, cyc);
+    run<kBitop3Dep2>(blocks, iters, out, cyc);
   }
   return 0;
 }
