@@ -43,7 +43,7 @@ typedef enum rs_status {
   RS_ERR_TOO_MANY_SHARDS = 9,          /* root.zig:242, 258 */
   RS_ERR_OUT_OF_MEMORY = 10,           /* allocator failure */
   RS_ERR_OVERFLOW = 11,                /* std.math.ceilPowerOfTwo */
-  RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO"); here only per-stripe patterns */
+  RS_ERR_LOW_RATE_UNSUPPORTED = 12,    /* root.zig:120, 227 @panic("TODO"); no longer returned (every path serves low-rate codes) */
   RS_ERR_SHARD_TAIL_UNSUPPORTED = 13,  /* root.zig:385 @panic("TODO"); no longer returned (tails are coded) */
   RS_ERR_INVALID_ARGUMENT = 14,        /* NULL pointer / bad stride */
   RS_ERR_DEVICE = 15,                  /* HIP runtime error (message: rs_last_error()) */

@@ -137,7 +137,7 @@ inline bool contig_ok(uint64_t shard_bytes, int nv) { return shard_bytes % (512u
 
 // Device-side plans for per-stripe erasure patterns (W entries per stripe)
 hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
-                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
+                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, bool low, const uint16_t *d_exp,
                                const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
                                RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s);
 

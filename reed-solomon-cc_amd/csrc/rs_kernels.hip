@@ -1039,23 +1039,33 @@ __device__ void fwht_lds(uint16_t *e, uint32_t m) {
   }
 }
 
-// per stripe: present[k+m] -> logs[W] (root.zig:277-289 + Generic.zig:200-215)
+// per stripe: present[k+m] -> logs[W] (root.zig:277-289 + Generic.zig:200-215). low: the
+// low-rate layout of rs_gf.cpp erasure_logs_low (C = ceilPow2(k): originals [0, k), known
+// zeros [k, C), recovery [C, C + m), unknown [C + m, W), transform over W)
 __global__ __launch_bounds__(1024) void k_erasure_logs(const uint8_t *__restrict__ present, uint64_t present_stride,
-                                                       uint32_t k, uint32_t m, uint32_t C, uint32_t W,
+                                                       uint32_t k, uint32_t m, uint32_t C, uint32_t W, uint32_t low,
                                                        const uint16_t *__restrict__ log_walsh,
                                                        uint16_t *__restrict__ logs) {
   __shared__ uint16_t e[65536];
   const uint8_t *pr = present + static_cast<uint64_t>(blockIdx.x) * present_stride;
-  const uint32_t end = C + k;
+  const uint32_t end = low ? C + m : C + k;
   for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x) {
     uint16_t v = 0;
-    if (i < m) v = pr[k + i] ? 0 : 1;
-    else if (i < C) v = 1;
-    else if (i < end) v = pr[i - C] ? 0 : 1;
+    if (low) {
+      if (i < k) v = pr[i] ? 0 : 1;
+      else if (i >= C && i < end) v = pr[k + i - C] ? 0 : 1;
+      else if (i >= end && i < W) v = 1;
+    } else if (i < m) {
+      v = pr[k + i] ? 0 : 1;
+    } else if (i < C) {
+      v = 1;
+    } else if (i < end) {
+      v = pr[i - C] ? 0 : 1;
+    }
     e[i] = v;
   }
   __syncthreads();
-  fwht_lds(e, end);
+  fwht_lds(e, low ? W : end);
   for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x) {
     const uint32_t prod = static_cast<uint32_t>(e[i]) * log_walsh[i];
     e[i] = static_cast<uint16_t>(add_mod_d(prod & 0xFFFF, prod >> 16));
@@ -1096,7 +1106,8 @@ __device__ void make_tab_d(RsTab &t, uint32_t lm, bool d1, const uint16_t *exp, 
 // per (stripe, position): masks, sources, restored slots (root.zig:291-326)
 __global__ __launch_bounds__(256) void k_pattern_tables(const uint8_t *__restrict__ present, uint64_t present_stride,
                                                         uint32_t k, uint32_t m, uint32_t C, uint32_t W, uint32_t n,
-                                                        uint32_t max_e, bool d1, const uint16_t *__restrict__ logs,
+                                                        uint32_t max_e, bool d1, uint32_t low,
+                                                        const uint16_t *__restrict__ logs,
                                                         const uint16_t *__restrict__ exp, const uint16_t *__restrict__ log,
                                                         RsTab *pre, RsTab *post, int32_t *src, int32_t *dst,
                                                         int32_t *status) {
@@ -1114,16 +1125,18 @@ __global__ __launch_bounds__(256) void k_pattern_tables(const uint8_t *__restric
   const uint32_t lm = logs[g];
   int32_t sv = -1, dv = -1;
   RsTab tp{}, tq{};
-  if (p < m && pr[k + p]) {
-    sv = kSrcRecovery | static_cast<int32_t>(p);
+  // positions: originals at o0 + i, recovery at r0 + r (low rate: o0 = 0, r0 = C)
+  const uint32_t o0 = low ? 0 : C, r0 = low ? C : 0;
+  if (p >= r0 && p < r0 + m && pr[k + p - r0]) {
+    sv = kSrcRecovery | static_cast<int32_t>(p - r0);
     make_tab_d(tp, lm, d1, exp, log);
-  } else if (p >= C && p < C + k && pr[p - C]) {
-    sv = static_cast<int32_t>(p - C);
+  } else if (p >= o0 && p < o0 + k && pr[p - o0]) {
+    sv = static_cast<int32_t>(p - o0);
     make_tab_d(tp, lm, d1, exp, log);
   }
-  if (p >= C && p < C + k && !pr[p - C]) {
+  if (p >= o0 && p < o0 + k && !pr[p - o0]) {
     int32_t slot = 0;
-    for (uint32_t i = 0; i < p - C; i++) slot += pr[i] ? 0 : 1;
+    for (uint32_t i = 0; i < p - o0; i++) slot += pr[i] ? 0 : 1;
     dv = slot < static_cast<int32_t>(max_e) ? slot : -1;
     make_tab_d(tq, 65535u - lm, d1, exp, log);
   }
@@ -1577,22 +1590,24 @@ hipError_t launch_pattern_matrix_impl(const uint8_t *d_present, uint64_t present
 }
 
 hipError_t launch_pattern_plan_impl(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m,
-                                    uint32_t C, uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
-                                    const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
+                                    uint32_t C, uint32_t W, uint64_t n, uint32_t max_e, bool d1, bool low,
+                                    const uint16_t *d_exp, const uint16_t *d_log, const uint16_t *d_log_walsh,
+                                    uint16_t *logs, RsTab *pre,
                                     RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
   trace_launch("k_erasure_logs");
   trace_launch("k_pattern_tables");
   for (uint64_t s0 = 0; s0 < n; s0 += 65535) {
     const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
     hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, d_present + s0 * present_stride,
-                       present_stride, k, m, C, W, d_log_walsh, logs + s0 * W);
+                       present_stride, k, m, C, W, low ? 1u : 0u, d_log_walsh, logs + s0 * W);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   const uint64_t total = n * W;
   const uint64_t blocks = (total + 255) / 256;
   hipLaunchKernelGGL(k_pattern_tables, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, d_present,
-                     present_stride, k, m, C, W, static_cast<uint32_t>(n), max_e, d1, logs, d_exp, d_log, pre, post,
+                     present_stride, k, m, C, W, static_cast<uint32_t>(n), max_e, d1, low ? 1u : 0u, logs, d_exp, d_log,
+                     pre, post,
                      src, dst, status);
   return hipGetLastError();
 }
@@ -1939,10 +1954,10 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
 }
 
 hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,
-                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, const uint16_t *d_exp,
+                               uint32_t W, uint64_t n, uint32_t max_e, bool d1, bool low, const uint16_t *d_exp,
                                const uint16_t *d_log, const uint16_t *d_log_walsh, uint16_t *logs, RsTab *pre,
                                RsTab *post, int32_t *src, int32_t *dst, int32_t *status, hipStream_t s) {
-  return launch_pattern_plan_impl(d_present, present_stride, k, m, C, W, n, max_e, d1, d_exp, d_log, d_log_walsh,
+  return launch_pattern_plan_impl(d_present, present_stride, k, m, C, W, n, max_e, d1, low, d_exp, d_log, d_log_walsh,
                                   logs, pre, post, src, dst, status, s);
 }
 
@@ -2071,7 +2086,7 @@ hipError_t launch_fdec_plan(const uint8_t *present, uint64_t present_stride, uin
   for (uint64_t s0 = 0; e == hipSuccess && s0 < n; s0 += 65535) {
     const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
     hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, trimmed + s0 * (k + m), static_cast<uint64_t>(k + m),
-                       k, m, C, W, d_log_walsh, logs + s0 * W);
+                       k, m, C, W, 0u, d_log_walsh, logs + s0 * W);
     e = hipGetLastError();
   }
   if (e != hipSuccess) return e;

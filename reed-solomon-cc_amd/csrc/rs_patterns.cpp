@@ -2,6 +2,8 @@
 // (§8 f2), the erasure locator and per-stripe plans built on the GPU.
 #include "rs_host.hpp"
 
+#include <unordered_map>
+
 using namespace rs;
 using namespace rs::host;
 
@@ -72,14 +74,32 @@ bool pdec_enabled() {
 // corrected multiply only (under D1 the literal decode is no inverse of the encode), and
 // no code whose D2 encode drops a chunk (its parity is no codeword, so the result would
 // depend on which recovery rows are read; root.zig:268-335 reads all of them)
-bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
+namespace {
+// decode_betas solves a small GF(2^16) system per code: memoised per (k, m), since every
+// reconstruct call asks
+bool has_decode_betas(uint64_t k, uint64_t m) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, bool> memo;
+  const uint64_t key = k << 32 | m;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+  }
   std::vector<uint16_t> beta;
+  const bool ok = fftnet::decode_betas(static_cast<uint32_t>(k), static_cast<uint32_t>(m), beta);
+  std::lock_guard<std::mutex> lk(mu);
+  memo[key] = ok;
+  return ok;
+}
+}  // namespace
+
+bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags) {
   const uint64_t C = ceil_pow2(m);
   const bool d2_drops = (flags & RS_FLAG_QUIRK_D2) && k > C && k % C == 0;
   return fdec_mode() != 0 && !(flags & RS_FLAG_QUIRK_D1) && !d2_drops && fft_enabled() &&
-         fftnet::supports(k, m, sb, true) &&
-         fftnet::pieces(sb) == 1 && sb % fftnet::kUnitBytes == 0 &&
-         fftnet::decode_betas(static_cast<uint32_t>(k), static_cast<uint32_t>(m), beta);
+         fftnet::supports(k, m, sb, true) && fftnet::pieces(sb) == 1 && sb % fftnet::kUnitBytes == 0 &&
+         has_decode_betas(k, m);
 }
 
 const jit::Kernel *wps_solve_kernel(WpsSlot &ws) {
@@ -204,7 +224,9 @@ extern "C" {
 
 const char *rs_patterns_kernel_name(uint64_t k, uint64_t m, size_t sb, uint32_t max_e, uint32_t flags) {
   thread_local std::string name;
-  if (psyn_enabled(k, m, sb, flags)) {
+  if (is_low_rate(k, m)) {
+    name = "pattern_fft_low";
+  } else if (psyn_enabled(k, m, sb, flags)) {
     name = "psyn_k" + std::to_string(k) + "_m" + std::to_string(m);
   } else if (fdec_patterns_enabled(k, m, sb, flags, max_e)) {
     name = "fft_decode";
@@ -228,9 +250,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
   TraceScope ts;
   return guarded([&]() -> int {
     int st = check_codec(k, m, sb);
-    if (st == RS_OK && is_low_rate(k, m))
-      return fail(RS_ERR_LOW_RATE_UNSUPPORTED, "per-stripe patterns: high-rate codes only");
     if (st) return st;
+    const bool low = is_low_rate(k, m);  // §8 f4: the low-rate layout on the FFT kernels only
     if (n_stripes == 0 || max_e == 0) return RS_OK;
     if (!d_present || !d_original || !d_recovery || !d_restored) return fail(RS_ERR_INVALID_ARGUMENT, "NULL pointer");
     if (present_stride == 0) present_stride = k + m;
@@ -274,12 +295,13 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     if (!max_nv) return fail(RS_ERR_INVALID_ARGUMENT, "device pointers/strides must be 4-byte aligned");
     int dev;
     if ((st = current_device(&dev))) return st;
-    const uint64_t C = ceil_pow2(m), W = ceil_pow2(C + k);
+    const uint64_t C = low ? ceil_pow2(k) : ceil_pow2(m), W = ceil_pow2(low ? C + m : C + k);
     const uint16_t *dexp, *dlog, *dlw;
     if ((st = device_tables(dev, &dexp, &dlog, &dlw))) return st;
+    if (low) flags &= ~(RS_FLAG_QUIRK_D1 | RS_FLAG_QUIRK_D2);  // no literal low-rate behaviour (rs_lowrate.cpp)
     // syndrome network (rs_psyn.hpp): the code's fixed k -> m network plus a per-stripe
     // e x e solve; corrected multiply, k <= 64, m <= 4, whole 4 KiB units
-    if (max_nv == 4 && psyn_enabled(k, m, sb, flags)) {
+    if (!low && max_nv == 4 && psyn_enabled(k, m, sb, flags)) {
       std::shared_ptr<PsynPlan> pp;
       if ((st = psyn_plan(dev, k, m, flags, pp))) return st;
       if (const jit::Kernel *pk = psyn_kernel(*pp)) {
@@ -302,7 +324,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     }
     // wide codes: the fused FFT reconstruct with per-stripe decode blocks built on the GPU
     // (trimmed rows R, erasure locator, masks)
-    if (max_nv == 4 && fdec_patterns_enabled(k, m, sb, flags, max_e)) {
+    if (!low && max_nv == 4 && fdec_patterns_enabled(k, m, sb, flags, max_e)) {
       std::shared_ptr<WpsSlot> ws;
       wps_slot(dev, k, m, flags, ws);
       const fftnet::Spec *dfs = nullptr;
@@ -346,7 +368,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       if (fdec_mode() == 1) return fail(RS_ERR_DEVICE, "RS_AMD_FDEC=1: fused FFT reconstruct kernel unavailable");
     }
     // wide codes: syndromes on the FFT kernel (per-stripe masks), then the e x e solve
-    if (max_nv == 4 && wps_enabled(k, m, sb, flags, max_e)) {
+    if (!low && max_nv == 4 && wps_enabled(k, m, sb, flags, max_e)) {
       std::shared_ptr<PsynPlan> pp;  // G and the Cantor basis
       if ((st = psyn_plan(dev, k, m, flags, pp))) return st;
       std::shared_ptr<WpsSlot> ws;
@@ -390,8 +412,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     hipStream_t s = static_cast<hipStream_t>(stream);
     // matrix path (below): corrected multiply, W <= 32, max_e <= 8
     const char *pm = std::getenv("RS_AMD_PATTERNS");
-    const bool use_matrix =
-        !literal_decode(k, m, flags) && W <= 32 && max_e <= kMatrixMaxOut && !(pm && std::string(pm) == "fft");
+    const bool use_matrix = !low && !literal_decode(k, m, flags) && W <= 32 && max_e <= kMatrixMaxOut &&
+                            !(pm && std::string(pm) == "fft");
     // per-stripe plan: logs u16 | pre RsTab | post RsTab | src i32 | dst i32 (W entries each)
     //                  [| trimmed present rows, matrix path]
     const uint64_t per = W * (2 + 2 * sizeof(RsTab) + 8);
@@ -416,8 +438,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     uint16_t *logs = reinterpret_cast<uint16_t *>(dst + n_stripes * W);
     hipError_t e = launch_pattern_plan(d_present, present_stride, static_cast<uint32_t>(k), static_cast<uint32_t>(m),
                                        static_cast<uint32_t>(C), static_cast<uint32_t>(W), n_stripes, max_e,
-                                       flags & RS_FLAG_QUIRK_D1, dexp, dlog, dlw, logs, pre, post, src, dst, d_status,
-                                       s);
+                                       flags & RS_FLAG_QUIRK_D1, low, dexp, dlog, dlw, logs, pre, post, src, dst,
+                                       d_status, s);
     if (e != hipSuccess) {
       (void)hipFreeAsync(tmp, s);
       return hip_fail(e, "launch_pattern_plan");
@@ -470,7 +492,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       if (e != hipSuccess) return hip_fail(e, "per-stripe matrix reconstruct");
       return RS_OK;
     }
-    const KernelChoice kc = choose_decode(k, m, sb, max_nv);
+    const KernelChoice kc = low ? choose_decode_w(W, sb, max_nv) : choose_decode(k, m, sb, max_nv);
     DecodeArgs a{};
     a.orig = static_cast<const uint8_t *>(d_original);
     a.orig_stripe_stride = orig_stride;
@@ -486,7 +508,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     a.pos_src = src;
     a.pos_dst = dst;
     a.work = static_cast<uint32_t>(W);
-    a.trunc = static_cast<uint32_t>(C + k);
+    a.trunc = static_cast<uint32_t>(low ? C + m : C + k);
+    a.trunc_fft = low ? static_cast<uint32_t>(k) : 0;  // as rs_lowrate.cpp low_reconstruct
     a.pattern_stride = W;
     a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
     if (kc.variant != Variant::kGeneric) {

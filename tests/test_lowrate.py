@@ -101,6 +101,7 @@ def test_low_rate_limits(monkeypatch):
     assert R.encode_kernel_name(16, 64, 1 << 16) == "net_encode_low_i16_o64"
     assert R.reconstruct_kernel_name(1000, 4000, 4096, [0] * 10 + [1] * 4990) == "decode_generic_nv1"
     assert R.reconstruct_kernel_name(3, 5, 4096, [0, 1, 1] + [1] * 5).startswith("net_reconstruct_low")
+    assert R.patterns_kernel_name(300, 1000, 4096, 300) == "pattern_fft_low"  # per-stripe patterns too
     monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
     assert R.encode_kernel_name(16, 64, 1 << 16) == "encode_low_reg_w16_nv1"
     monkeypatch.setenv("RS_AMD_JIT", "0")
@@ -270,3 +271,45 @@ def test_low_rate_encode_scratch_cap(oracle, monkeypatch, cap_mb):
     for s in range(n):
         st, exp = oracle.encode_low(k, m, data[s])
         assert st == 0 and np.array_equal(got[s], exp), s
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("k,m,sb", [(3, 5, 64), (5, 9, 100), (10, 20, 4096), (17, 130, 192), (100, 600, 2048), (300, 1000, 4096)])
+def test_low_rate_per_stripe_patterns(oracle, k, m, sb):
+    """rs_reconstruct_batch_dev_patterns on low-rate codes (round 3 rejected them): one
+    erasure pattern per stripe, originals and recovery shards lost, stripe 0 with exactly k
+    present, one stripe with too few (NotEnoughShards, nothing written), and restored slots
+    past each stripe's losses left alone. Encode checked against rso_encode_low; the
+    reconstruct of an MDS code is unique, so the lost data is the expectation."""
+    n = 6
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(k * 31 + m + sb)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev)
+    par = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
+    R.encode_batch_dev(k, m, d, par)
+    torch.cuda.synchronize()
+    st, exp0 = oracle.encode_low(k, m, data[0])
+    assert st == 0 and np.array_equal(par[0].cpu().numpy(), exp0)
+    present = np.ones((n, k + m), np.uint8)
+    for s in range(n):
+        e = k if s == 0 else int(rng.integers(1, k + 1))
+        present[s, rng.choice(k, size=e, replace=False)] = 0
+        extra = m - e if s == 0 else int(rng.integers(0, m - e + 1))
+        present[s, k + rng.choice(m, size=extra, replace=False)] = 0
+    present[n - 1, :] = 0
+    present[n - 1, k + m - (k - 1):] = 1  # k - 1 present
+    max_e = k
+    out = torch.full((n, max_e, sb), 0xAB, dtype=torch.uint8, device=dev)
+    status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    assert R.patterns_kernel_name(k, m, sb, max_e) == "pattern_fft_low"
+    R.reconstruct_batch_dev_patterns(k, m, torch.from_numpy(present).to(dev), d, par, out, status)
+    torch.cuda.synchronize()
+    out, status = out.cpu().numpy(), status.cpu().numpy()
+    for s in range(n - 1):
+        missing = [i for i in range(k) if not present[s, i]]
+        assert status[s] == 0, s
+        assert np.array_equal(out[s, :len(missing)], data[s, missing]), (s, missing)
+        assert (out[s, len(missing):] == 0xAB).all(), s
+    assert status[n - 1] == 2  # RS_ERR_NOT_ENOUGH_SHARDS
