@@ -363,9 +363,10 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       HIP_TRY(launch_decode(kc, a, s));
       return RS_OK;
     }
-    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
+    // launch_decode_generic: X and Y, W positions each
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (2ull * plan->work * sb)));
     void *scratch = nullptr;
-    HIP_TRY(hipMallocAsync(&scratch, per * plan->work * sb, s));
+    HIP_TRY(hipMallocAsync(&scratch, per * 2ull * plan->work * sb, s));
     for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
       DecodeArgs b = a;
       b.orig += s0 * orig_stride;

@@ -57,7 +57,7 @@ struct DecodeArgs {
   uint32_t work;   // W
   uint32_t trunc;  // chunk + k (IFFT truncation; the FFT's too unless trunc_fft is set)
   uint32_t trunc_fft = 0;  // low rate: FFT truncated to k (only positions [0, k) are read)
-  uint8_t *scratch;  // generic path only: [stripe][W][sb]
+  uint8_t *scratch;  // generic path only: [stripe][2W][sb] (launch_decode_generic)
   uint64_t scratch_stripes;
   // matrix variant: restored[j] = XOR_i map_ij(in[i]) over n_in received shards
   // pos_src[0..n_in) = sources, tab_mat[i * n_out + j] = map_ij (GF(2)-linear)

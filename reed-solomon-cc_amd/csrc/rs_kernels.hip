@@ -12,9 +12,10 @@
 //  * k_decode_reg<W, NV>: fused reconstruct, the W-point transforms in VGPRs.
 //    Reads the k+m-e received shards it needs, writes the e restored ones.
 //    Mirrors Decoder.decode (root.zig:268-335).
-//  * k_encode_generic / k_decode_generic: the same codec for any (k, m), each
-//    lane walking its column through a global scratch work buffer
-//    [stripe][W][shard_bytes] (the reference's Shards layout, root.zig:350-395).
+//  * k_encode_generic / launch_decode_generic: the same codec for any (k, m) through
+//    a global scratch work buffer [stripe][W][shard_bytes] (the reference's Shards
+//    layout, root.zig:350-395); the decode as a sequence of launches whose grid spans
+//    the transform's positions (k_dec_gather, k_phase, k_dec_deriv, k_dec_scatter).
 //  * k_engine_transform / k_mul_scalar: the Engine seam (Generic.zig) as test shims.
 #include <hip/hip_runtime.h>
 
@@ -851,73 +852,116 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
 
 // Formal derivative (root.zig:306-312): for i in [1, W), w[i - lowbit(i) + j] ^= w[i + j]
 // for j < lowbit(i). Reads lie at or above i and writes below it, so every read sees an
-// original value: out[p] = in[p] ^ XOR over clear bits b of p (b < log2 W) of in[p + 2^b].
-// Walked in 64-position blocks, ascending (every position a block reads lies above it, so
-// it is still original): the low 6 bits combine in VGPRs (ascending, the same argument),
-// the high bits add the partner blocks blk + 2^b. One independent load per term instead of
-// a dependent load-load-store chain per term.
-template <int NV>
-__device__ __forceinline__ void deriv_mem(uint8_t *w, uint32_t off, uint64_t ps, uint64_t W) {
-  const uint64_t B = W < 64 ? W : 64;
-  for (uint64_t blk = 0; blk < W; blk += B) {
-    Sym<NV> s[64];
-#pragma unroll
-    for (int l = 0; l < 64; l++)
-      if (static_cast<uint64_t>(l) < B) ldb(s[l], row_rsrc(w + (blk + l) * ps), off);
-#pragma unroll
-    for (int l = 0; l < 64; l++)
-#pragma unroll
-      for (int b = 0; b < 6; b++)
-        if (!((l >> b) & 1) && static_cast<uint64_t>(l + (1 << b)) < B) dev::xor_into(s[l], s[l + (1 << b)]);
-    for (uint64_t d = B; d < W; d <<= 1) {
-      if (blk & d) continue;
-#pragma unroll
-      for (int l = 0; l < 64; l++) {
-        Sym<NV> t;
-        ldb(t, row_rsrc(w + (blk + d + l) * ps), off);  // B == 64 here
-        dev::xor_into(s[l], t);
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < 64; l++)
-      if (static_cast<uint64_t>(l) < B) stb(row_rsrc(w + (blk + l) * ps), off, s[l]);
-  }
-}
+// original value: out[p] = in[p] ^ XOR over clear bits b of p (b < log2 W) of in[p + 2^b]
+// (k_dec_deriv: 64-position blocks, the low 6 bits combined in VGPRs in ascending order,
+// the high bits as partner blocks; one independent load per term).
 
-template <int NV>
-__global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
+// ---- the generic reconstruct as a launch sequence (launch_decode_generic): the same steps
+// as k_decode_generic with the positions spread over the grid (y) instead of walked by one
+// lane, so a small batch still fills the chip. Scratch [stripe][2W][sb]: X = [0, W), Y = [W, 2W).
+// Grid: x = column units, y = position block / phase sub-problem, z = stripes (strided).
+constexpr uint32_t kDecBlock = 64;  // positions per gather / derivative / scatter thread
+
+__global__ __launch_bounds__(kBlock) void k_dec_gather(DecodeArgs a) {
   uint32_t off;
-  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
-  const uint64_t sb = a.shard_bytes, W = a.work;
-  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
+  if (!lane_offset<1>(a.shard_bytes, false, off)) return;
+  const uint64_t sb = a.shard_bytes, W = a.work, p0 = static_cast<uint64_t>(blockIdx.y) * kDecBlock;
+  for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
     const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
     const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
-    uint8_t *work = a.scratch + s * W * sb + off;
-    const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride, *tab_post = a.tab_post + s * a.pattern_stride;
-    const int32_t *pos_src = a.pos_src + s * a.pattern_stride, *pos_dst = a.pos_dst + s * a.pattern_stride;
-    for (uint64_t p = 0; p < W; p++) {
+    uint8_t *x = a.scratch + s * 2 * W * sb;
+    const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride;
+    const int32_t *pos_src = a.pos_src + s * a.pattern_stride;
+    for (uint64_t p = p0; p < p0 + kDecBlock && p < W; p++) {
       const int32_t src = ((const __attribute__((address_space(4))) int32_t *)pos_src)[p];
-      Sym<NV> v;
+      Sym<1> v;
       if (src >= 0) {
         const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, a.contig);
+        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, false);
         dev::mul_inplace(v, dev::load_tab(tab_pre + p));
       } else {
         dev::zero(v);
       }
-      st(work + p * sb, v);
+      stb(row_rsrc(x + p * sb), off, v);
     }
-    ifft_mem<NV>(work - off, off, sb, W, a.trunc, a.tab_ifft);
-    deriv_mem<NV>(work - off, off, sb, W);
-    fft_mem<NV>(work - off, off, sb, W, a.trunc_fft ? a.trunc_fft : a.trunc, a.tab_fft);
-    uint8_t *out = a.out + s * a.out_stripe_stride + off;
-    for (uint64_t p = 0; p < W; p++) {
+  }
+}
+
+struct PhaseArgs {
+  uint8_t *buf;  // stripe s's transform: buf + s * stripe_stride, position p at + p * sb
+  uint64_t stripe_stride, sb, n_stripes, size, rmax, ti;
+  const RsTab *tabs;
+  uint32_t dlo_log;
+};
+
+// one phase of xform_ph (same schedule), sub-problem blockIdx.y, in place
+template <int N, bool INV>
+__global__ __launch_bounds__(kBlock) void k_phase(PhaseArgs a) {
+  uint32_t off;
+  if (!lane_offset<1>(a.sb, false, off)) return;
+  const uint64_t sub = blockIdx.y, dmask = (1ull << a.dlo_log) - 1;
+  const uint64_t blk = (sub >> a.dlo_log) * (static_cast<uint64_t>(N) << a.dlo_log), lo = sub & dmask;
+  for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    uint8_t *b = a.buf + s * a.stripe_stride;
+    Sym<1> v[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) ldb(v[j], row_rsrc(b + (blk + lo + (static_cast<uint64_t>(j) << a.dlo_log)) * a.sb), off);
+    if constexpr (INV) ifft_sub<N, 1>(v, a.tabs, a.ti, a.size, a.rmax, blk, a.dlo_log);
+    else fft_sub<N, 1>(v, a.tabs, a.ti, a.size, a.rmax, blk, a.dlo_log);
+#pragma unroll
+    for (int j = 0; j < N; j++) stb(row_rsrc(b + (blk + lo + (static_cast<uint64_t>(j) << a.dlo_log)) * a.sb), off, v[j]);
+  }
+}
+
+// formal derivative X -> Y (deriv_mem's formula; out of place, so the blocks run in parallel)
+__global__ __launch_bounds__(kBlock) void k_dec_deriv(DecodeArgs a) {
+  uint32_t off;
+  if (!lane_offset<1>(a.shard_bytes, false, off)) return;
+  const uint64_t sb = a.shard_bytes, W = a.work, B = W < kDecBlock ? W : kDecBlock;
+  const uint64_t blk = static_cast<uint64_t>(blockIdx.y) * B;
+  for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    const uint8_t *x = a.scratch + s * 2 * W * sb;
+    uint8_t *y = a.scratch + (s * 2 + 1) * W * sb;
+    Sym<1> v[kDecBlock];
+#pragma unroll
+    for (int l = 0; l < static_cast<int>(kDecBlock); l++)
+      if (static_cast<uint64_t>(l) < B) ldb(v[l], row_rsrc(x + (blk + l) * sb), off);
+#pragma unroll
+    for (int l = 0; l < static_cast<int>(kDecBlock); l++)
+#pragma unroll
+      for (int b = 0; b < 6; b++)
+        if (!((l >> b) & 1) && static_cast<uint64_t>(l + (1 << b)) < B) dev::xor_into(v[l], v[l + (1 << b)]);
+    for (uint64_t d = B; d < W; d <<= 1) {
+      if (blk & d) continue;
+#pragma unroll
+      for (int l = 0; l < static_cast<int>(kDecBlock); l++) {
+        Sym<1> t;
+        ldb(t, row_rsrc(x + (blk + d + l) * sb), off);  // B == 64 here
+        dev::xor_into(v[l], t);
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < static_cast<int>(kDecBlock); l++)
+      if (static_cast<uint64_t>(l) < B) stb(row_rsrc(y + (blk + l) * sb), off, v[l]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dec_scatter(DecodeArgs a) {
+  uint32_t off;  // the split lane layout of the scratch (generic launches have a.contig false)
+  if (!lane_offset<1>(a.shard_bytes, false, off)) return;
+  const uint64_t sb = a.shard_bytes, W = a.work, p0 = static_cast<uint64_t>(blockIdx.y) * kDecBlock;
+  for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    const uint8_t *y = a.scratch + (s * 2 + 1) * W * sb;
+    uint8_t *out = a.out + s * a.out_stripe_stride;
+    const RsTab *tab_post = a.tab_post + s * a.pattern_stride;
+    const int32_t *pos_dst = a.pos_dst + s * a.pattern_stride;
+    for (uint64_t p = p0; p < p0 + kDecBlock && p < W; p++) {
       const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
       if (dst >= 0) {
-        Sym<NV> v;
-        ld(v, work + p * sb);
+        Sym<1> v;
+        ldb(v, row_rsrc(y + p * sb), off);
         dev::mul_inplace(v, dev::load_tab(tab_post + p));
-        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, 0u, v, a.contig);
+        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, off, v, false);
       }
     }
   }
@@ -1895,6 +1939,62 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
   return hipGetLastError();
 }
 
+// the phases of xform_ph (same grouping), each a launch of k_phase over every sub-problem
+static hipError_t launch_phases(uint8_t *buf, uint64_t stripe_stride, uint64_t sb, uint64_t n, uint64_t size,
+                                uint64_t trunc, const RsTab *tabs, bool inv, hipStream_t s) {
+  uint32_t lg = 0;
+  while ((1ull << lg) < size) lg++;
+  const uint32_t n4 = lg / 2;
+  const bool r2 = lg & 1;
+  PhaseArgs pa{buf, stripe_stride, sb, n, size, trunc < size ? trunc : size, 0, tabs, 0};
+  const dim3 g0 = grid_for(sb, 1, 1);
+  const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(n, 65535));
+  uint32_t layer = 0;
+  bool r2_done = !r2;
+  do {
+    const uint32_t c = std::min<uint32_t>(3, n4 - layer);
+    const bool with_r2 = !r2_done && layer + c == n4 && c < 3;
+    const uint32_t nn = (1u << (2 * c)) << (with_r2 ? 1 : 0);
+    pa.dlo_log = inv ? 2 * layer : (with_r2 || c == 0 ? 0 : lg - 2 * (layer + c));
+    const dim3 g(g0.x, static_cast<uint32_t>(size / nn), gz);
+#define RS_PH_CASE(N_)                                                                         \
+  case N_:                                                                                     \
+    if (inv) hipLaunchKernelGGL((k_phase<N_, true>), g, dim3(kBlock), 0, s, pa);              \
+    else hipLaunchKernelGGL((k_phase<N_, false>), g, dim3(kBlock), 0, s, pa);                 \
+    break;
+    switch (nn) {
+      RS_PH_CASE(1) RS_PH_CASE(2) RS_PH_CASE(4) RS_PH_CASE(8) RS_PH_CASE(16) RS_PH_CASE(32) RS_PH_CASE(64)
+      default: return hipErrorInvalidValue;
+    }
+#undef RS_PH_CASE
+    if (hipError_t e = hipGetLastError()) return e;
+    for (uint32_t l = layer; l < layer + c; l++) pa.ti += inv ? 3 * (size >> (2 * l + 2)) : 3ull << (2 * l);
+    layer += c;
+    r2_done = r2_done || with_r2 || c == 0;
+  } while (layer < n4 || !r2_done);
+  return hipSuccess;
+}
+
+// Decoder.decode (root.zig:268-335) over any W: gather * pre -> IFFT -> derivative -> FFT ->
+// * post -> scatter, five stages of launches (a.scratch: 2W positions per stripe)
+static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
+  const uint64_t W = a.work, sb = a.shard_bytes;
+  if (W == 0 || (W & (W - 1)) || W / kDecBlock > 65535 || sb % 64) return hipErrorInvalidValue;
+  const dim3 g0 = grid_for(sb, 1, 1);
+  const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
+  const dim3 gb(g0.x, static_cast<uint32_t>((W + kDecBlock - 1) / kDecBlock), gz);
+  hipLaunchKernelGGL(k_dec_gather, gb, dim3(kBlock), 0, s, a);
+  if (hipError_t e = hipGetLastError()) return e;
+  if (hipError_t e = launch_phases(a.scratch, 2 * W * sb, sb, a.n_stripes, W, a.trunc, a.tab_ifft, true, s)) return e;
+  hipLaunchKernelGGL(k_dec_deriv, gb, dim3(kBlock), 0, s, a);
+  if (hipError_t e = hipGetLastError()) return e;
+  if (hipError_t e = launch_phases(a.scratch + W * sb, 2 * W * sb, sb, a.n_stripes, W,
+                                   a.trunc_fft ? a.trunc_fft : a.trunc, a.tab_fft, false, s))
+    return e;
+  hipLaunchKernelGGL(k_dec_scatter, gb, dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
 static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
   const dim3 grid = grid_for(a.shard_bytes, kc.nv, a.n_stripes);
   if (kc.variant == Variant::kRegister) {
@@ -1919,8 +2019,7 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
     RS_MAT_NV(5) RS_MAT_NV(6) RS_MAT_NV(7) RS_MAT_NV(8)
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(k_decode_generic<1>, grid, dim3(kBlock), 0, s, a);
-  return hipGetLastError();
+  return launch_decode_generic(a, s);
 }
 
 hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,

@@ -479,9 +479,10 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
       a.n_stripes = n_stripes;
       e = launch_decode(kc, a, s);
     } else {
-      const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (W * sb)));
+      // launch_decode_generic: X and Y, W positions each
+      const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (2ull * W * sb)));
       void *scratch = nullptr;
-      e = hipMallocAsync(&scratch, cap * W * sb, s);
+      e = hipMallocAsync(&scratch, cap * 2ull * W * sb, s);
       for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += cap) {
         DecodeArgs b = a;
         b.orig += s0 * orig_stride;
