@@ -375,9 +375,11 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
       HIP_TRY(launch_decode(kc, a, s));
       return RS_OK;
     }
-    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, kScratchCap / (plan->work * sb)));
+    // launch_decode_generic: the transform plus the FFT's kept rows, per stripe
+    const uint64_t rows = decode_generic_rows(plan->work, a.trunc, a.trunc_fft);
+    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, scratch_cap() / (rows * sb)));
     void *scratch = nullptr;
-    HIP_TRY(dev_malloc_async(&scratch, per * plan->work * sb, s));
+    HIP_TRY(dev_malloc_async(&scratch, per * rows * sb, s));
     for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {
       DecodeArgs b = a;
       b.orig += s0 * orig_stride;

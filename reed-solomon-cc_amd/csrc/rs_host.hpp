@@ -235,7 +235,7 @@ int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out
 int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft);
 
 constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
-// the low-rate generic kernels' cap: kScratchCap, or RS_AMD_SCRATCH_CAP_MB (tests)
+// the generic kernels' scratch cap per launch: kScratchCap, or RS_AMD_SCRATCH_CAP_MB
 inline uint64_t scratch_cap() {
   const char *e = std::getenv("RS_AMD_SCRATCH_CAP_MB");
   return e && *e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20 : kScratchCap;

@@ -71,7 +71,7 @@ struct DecodeArgs {
   uint32_t work;   // W
   uint32_t trunc;  // chunk + k (IFFT truncation; the FFT's too unless trunc_fft is set)
   uint32_t trunc_fft = 0;  // low rate: FFT truncated to k (only positions [0, k) are read)
-  uint8_t *scratch;  // generic path only: [stripe][W][sb]
+  uint8_t *scratch;  // generic path only: [stripe][decode_generic_rows][sb] (launch_decode_generic)
   uint64_t scratch_stripes;
   // matrix variant: restored[j] = XOR_i map_ij(in[i]) over n_in received shards
   // pos_src[0..n_in) = sources, tab_mat[i * n_out + j] = map_ij (GF(2)-linear)
@@ -112,6 +112,8 @@ struct KernelChoice {
 // max_nv: widest per-lane access (1, 2, 4 dword pairs) the pointer/stride alignment allows
 KernelChoice choose_encode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
 KernelChoice choose_decode(uint64_t k, uint64_t m, uint64_t shard_bytes, int max_nv);
+// scratch positions per stripe of the generic reconstruct (W transform + the FFT's kept rows)
+uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft);
 KernelChoice choose_decode_w(uint64_t W, uint64_t shard_bytes, int max_nv);  // by transform size
 
 // Low-rate encode (rs_gf.hpp scalar_encode_low): EncodeArgs with chunk = C = ceilPow2(k),

@@ -12,9 +12,10 @@
 //  * k_decode_reg<W, NV>: fused reconstruct, the W-point transforms in VGPRs.
 //    Reads the k+m-e received shards it needs, writes the e restored ones.
 //    Mirrors Decoder.decode (root.zig:268-335).
-//  * k_encode_generic / k_decode_generic: the same codec for any (k, m), each
-//    lane walking its column through a global scratch work buffer
-//    [stripe][W][shard_bytes] (the reference's Shards layout, root.zig:350-395).
+//  * k_encode_generic / launch_decode_generic: the same codec for any (k, m) through
+//    a global scratch work buffer [stripe][W][shard_bytes] (the reference's Shards
+//    layout, root.zig:350-395); the decode as a sequence of launches whose grid spans
+//    the transform's positions (k_dec_gather, k_phase, k_dec_deriv, k_dec_scatter).
 //  * k_engine_transform / k_mul_scalar: the Engine seam (Generic.zig) as test shims.
 #include <hip/hip_runtime.h>
 
@@ -22,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "rs_device.hpp"
 #include "rs_internal.hpp"
@@ -851,73 +853,111 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
 
 // Formal derivative (root.zig:306-312): for i in [1, W), w[i - lowbit(i) + j] ^= w[i + j]
 // for j < lowbit(i). Reads lie at or above i and writes below it, so every read sees an
-// original value: out[p] = in[p] ^ XOR over clear bits b of p (b < log2 W) of in[p + 2^b].
-// Walked in 64-position blocks, ascending (every position a block reads lies above it, so
-// it is still original): the low 6 bits combine in VGPRs (ascending, the same argument),
-// the high bits add the partner blocks blk + 2^b. One independent load per term instead of
-// a dependent load-load-store chain per term.
-template <int NV>
-__device__ __forceinline__ void deriv_mem(uint8_t *w, uint32_t off, uint64_t ps, uint64_t W) {
-  const uint64_t B = W < 64 ? W : 64;
-  for (uint64_t blk = 0; blk < W; blk += B) {
-    Sym<NV> s[64];
-#pragma unroll
-    for (int l = 0; l < 64; l++)
-      if (static_cast<uint64_t>(l) < B) ldb(s[l], row_rsrc(w + (blk + l) * ps), off);
-#pragma unroll
-    for (int l = 0; l < 64; l++)
-#pragma unroll
-      for (int b = 0; b < 6; b++)
-        if (!((l >> b) & 1) && static_cast<uint64_t>(l + (1 << b)) < B) dev::xor_into(s[l], s[l + (1 << b)]);
-    for (uint64_t d = B; d < W; d <<= 1) {
-      if (blk & d) continue;
-#pragma unroll
-      for (int l = 0; l < 64; l++) {
-        Sym<NV> t;
-        ldb(t, row_rsrc(w + (blk + d + l) * ps), off);  // B == 64 here
-        dev::xor_into(s[l], t);
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < 64; l++)
-      if (static_cast<uint64_t>(l) < B) stb(row_rsrc(w + (blk + l) * ps), off, s[l]);
-  }
-}
+// original value: out[p] = in[p] ^ XOR over clear bits b of p (b < log2 W) of in[p + 2^b]
+// (k_dec_deriv: 64-position blocks, the low 6 bits combined in VGPRs in ascending order,
+// the high bits as partner blocks; one independent load per term).
 
-template <int NV>
-__global__ __launch_bounds__(kBlock) void k_decode_generic(DecodeArgs a) {
+// ---- the generic reconstruct as a launch sequence (launch_decode_generic): one launch per
+// phase of xform_ph, the phase's sub-problems across the grid (y), so a small batch still
+// fills the chip. Grid: x = column units, y = sub-problem, z = stripes (strided).
+// Per stripe the scratch holds X (W positions: the IFFT, in place) and Y (the positions the
+// truncated FFT still needs, decode_generic_rows). The steps ride on the phases:
+//  * GATHER (first IFFT phase): positions come from the received shards * pre, zero where
+//    nothing was received (root.zig:291-303), instead of a staging pass;
+//  * the IFFT writes only positions < round_up(trunc, span): a sub-problem past the
+//    truncation is all zero and so is what it would write (the next phase reads zeros);
+//  * DERIV (first FFT phase, X -> Y): the formal derivative (root.zig:306-312) as
+//    out[p] = in[p] ^ XOR over clear bits b of p of in[p + 2^b] (every read an original
+//    value: a sum of shifted copies of X). The phase spans every position, so bits the
+//    sub-problem holds combine in VGPRs (ascending, reads above writes); the low bits
+//    (b < dlo_log) are partner loads from X, which this phase does not write;
+//  * the FFT writes only positions < round_up(trunc_fft, span) and skips sub-problems past
+//    the truncation (their outputs feed nothing: root.zig:318 reads [0, trunc));
+//  * SCATTER (last FFT phase): only the erased positions, * post, into the restored rows
+//    (root.zig:320-326).
+enum : int { kPhGather = 1, kPhDeriv = 2, kPhScatter = 4 };
+
+struct PhaseArgs {
+  const uint8_t *src;  // stripe s's input: src + s * src_stride, position p at + p * sb
+  uint8_t *dst;        // output (in place: dst == src)
+  uint64_t src_stride, dst_stride, n_src, n_dst;  // positions >= n_src read as zero, >= n_dst not stored
+  uint64_t sb, size, rmax, ti;
+  const RsTab *tabs;
+  uint32_t dlo_log;
+};
+
+template <int N, bool INV, int MODE>
+__global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
   uint32_t off;
-  if (!lane_offset<NV>(a.shard_bytes, a.contig, off)) return;
-  const uint64_t sb = a.shard_bytes, W = a.work;
-  for (uint64_t s = blockIdx.y; s < a.n_stripes; s += gridDim.y) {
-    const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
-    const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
-    uint8_t *work = a.scratch + s * W * sb + off;
-    const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride, *tab_post = a.tab_post + s * a.pattern_stride;
-    const int32_t *pos_src = a.pos_src + s * a.pattern_stride, *pos_dst = a.pos_dst + s * a.pattern_stride;
-    for (uint64_t p = 0; p < W; p++) {
-      const int32_t src = ((const __attribute__((address_space(4))) int32_t *)pos_src)[p];
-      Sym<NV> v;
-      if (src >= 0) {
-        const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-        dev::load_sym(v, base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, a.contig);
-        dev::mul_inplace(v, dev::load_tab(tab_pre + p));
-      } else {
-        dev::zero(v);
+  if (!lane_offset<1>(q.sb, false, off)) return;
+  const uint64_t sb = q.sb, sub = blockIdx.y, dlo = 1ull << q.dlo_log;
+  const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
+  for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    Sym<1> v[N];
+    if constexpr ((MODE & kPhGather) != 0) {
+      const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
+      const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+      const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride;
+      const int32_t *pos_src = a.pos_src + s * a.pattern_stride;
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        const int32_t src = p < q.n_src ? ((const __attribute__((address_space(4))) int32_t *)pos_src)[p] : -1;
+        if (src >= 0) {
+          const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
+          dev::load_sym(v[j], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, false);
+          dev::mul_inplace(v[j], dev::load_tab(tab_pre + p));
+        } else {
+          dev::zero(v[j]);
+        }
       }
-      st(work + p * sb, v);
+    } else {
+      const uint8_t *x = q.src + s * q.src_stride;
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p < q.n_src) ldb(v[j], row_rsrc(x + p * sb), off);
+        else dev::zero(v[j]);
+      }
+      if constexpr ((MODE & kPhDeriv) != 0) {
+#pragma unroll
+        for (int j = 0; j < N; j++)
+#pragma unroll
+          for (int bb = 1; bb < N; bb <<= 1)
+            if (!(j & bb)) dev::xor_into(v[j], v[j + bb]);
+        for (uint32_t b = 0; b < q.dlo_log; b++) {
+          if ((lo >> b) & 1) continue;  // wave-uniform
+#pragma unroll
+          for (int j = 0; j < N; j++) {
+            Sym<1> t;
+            ldb(t, row_rsrc(x + (blk + lo + (1ull << b) + (static_cast<uint64_t>(j) << q.dlo_log)) * sb), off);
+            dev::xor_into(v[j], t);
+          }
+        }
+      }
     }
-    ifft_mem<NV>(work - off, off, sb, W, a.trunc, a.tab_ifft);
-    deriv_mem<NV>(work - off, off, sb, W);
-    fft_mem<NV>(work - off, off, sb, W, a.trunc_fft ? a.trunc_fft : a.trunc, a.tab_fft);
-    uint8_t *out = a.out + s * a.out_stripe_stride + off;
-    for (uint64_t p = 0; p < W; p++) {
-      const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
-      if (dst >= 0) {
-        Sym<NV> v;
-        ld(v, work + p * sb);
-        dev::mul_inplace(v, dev::load_tab(tab_post + p));
-        dev::store_sym(out + static_cast<uint64_t>(dst) * sb, 0u, v, a.contig);
+    if constexpr (INV) ifft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+    else fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+    if constexpr ((MODE & kPhScatter) != 0) {
+      uint8_t *out = a.out + s * a.out_stripe_stride;
+      const RsTab *tab_post = a.tab_post + s * a.pattern_stride;
+      const int32_t *pos_dst = a.pos_dst + s * a.pattern_stride;
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p >= q.rmax) continue;
+        const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
+        if (dst >= 0) {
+          dev::mul_inplace(v[j], dev::load_tab(tab_post + p));
+          dev::store_sym(out + static_cast<uint64_t>(dst) * sb, off, v[j], false);
+        }
+      }
+    } else {
+      uint8_t *y = q.dst + s * q.dst_stride;
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p < q.n_dst) stb(row_rsrc(y + p * sb), off, v[j]);
       }
     }
   }
@@ -1925,6 +1965,93 @@ static hipError_t launch_encode_one(const KernelChoice &kc, const EncodeArgs &a,
   return hipGetLastError();
 }
 
+// the phases of xform_ph (same grouping): size N, lowest distance 2^dlo_log, first table
+struct XPhase {
+  uint32_t n, dlo_log;
+  uint64_t ti;
+};
+static void xform_phases(uint64_t size, bool inv, std::vector<XPhase> &out) {
+  uint32_t lg = 0;
+  while ((1ull << lg) < size) lg++;
+  const uint32_t n4 = lg / 2;
+  uint32_t layer = 0;
+  bool r2_done = !(lg & 1);
+  uint64_t ti = 0;
+  out.clear();
+  do {
+    const uint32_t c = std::min<uint32_t>(3, n4 - layer);
+    const bool with_r2 = !r2_done && layer + c == n4 && c < 3;
+    const uint32_t nn = (1u << (2 * c)) << (with_r2 ? 1 : 0);
+    out.push_back({nn, inv ? 2 * layer : (with_r2 || c == 0 ? 0 : lg - 2 * (layer + c)), ti});
+    for (uint32_t l = layer; l < layer + c; l++) ti += inv ? 3 * (size >> (2 * l + 2)) : 3ull << (2 * l);
+    layer += c;
+    r2_done = r2_done || with_r2 || c == 0;
+  } while (layer < n4 || !r2_done);
+}
+
+static uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+// positions of the FFT's Y buffer: those the phases after the first read (0 for one phase)
+static uint64_t decode_y_rows(uint64_t W, uint64_t rmax_fft) {
+  std::vector<XPhase> ph;
+  xform_phases(W, false, ph);
+  return ph.size() > 1 ? std::min(W, round_up(rmax_fft, 1ull << ph[0].dlo_log)) : 0;
+}
+
+uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft) {
+  return W + decode_y_rows(W, trunc_fft ? trunc_fft : trunc);
+}
+
+template <bool INV, int MODE>
+static hipError_t launch_dphase(uint32_t n, dim3 g, const DecodeArgs &a, const PhaseArgs &q, hipStream_t s) {
+  switch (n) {
+#define RS_DPH_CASE(N_) \
+  case N_: hipLaunchKernelGGL((k_dphase<N_, INV, MODE>), g, dim3(kBlock), 0, s, a, q); break;
+    RS_DPH_CASE(2) RS_DPH_CASE(4) RS_DPH_CASE(8) RS_DPH_CASE(16) RS_DPH_CASE(32) RS_DPH_CASE(64)
+#undef RS_DPH_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// Decoder.decode (root.zig:268-335) over any W as one launch per transform phase
+// (a.scratch: decode_generic_rows positions per stripe)
+static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
+  const uint64_t W = a.work, sb = a.shard_bytes;
+  if (W < 2 || (W & (W - 1)) || W > 65536 || sb % 64) return hipErrorInvalidValue;
+  const uint64_t ri = std::min<uint64_t>(a.trunc, W), rf = std::min<uint64_t>(a.trunc_fft ? a.trunc_fft : a.trunc, W);
+  const uint64_t ylen = decode_y_rows(W, rf), stride = (W + ylen) * sb;
+  uint8_t *X = a.scratch, *Y = a.scratch + W * sb;
+  const dim3 g0 = grid_for(sb, 1, 1);
+  const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
+  std::vector<XPhase> ph;
+  xform_phases(W, true, ph);
+  uint64_t lim = 0;  // positions the previous IFFT phase wrote (the rest are zero)
+  for (size_t i = 0; i < ph.size(); i++) {
+    const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(ri, span);
+    PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[i].ti, a.tab_ifft, ph[i].dlo_log};
+    const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
+    hipError_t e = i == 0 ? launch_dphase<true, kPhGather>(ph[i].n, g, a, q, s)
+                          : launch_dphase<true, 0>(ph[i].n, g, a, q, s);
+    if (e != hipSuccess) return e;
+    lim = wl;
+  }
+  xform_phases(W, false, ph);
+  for (size_t i = 0; i < ph.size(); i++) {
+    const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(rf, span);
+    const bool first = i == 0, last = i + 1 == ph.size();
+    PhaseArgs q{first ? X : Y, Y, stride, stride, first ? W : ylen, ylen, sb, W, rf, ph[i].ti, a.tab_fft,
+                ph[i].dlo_log};
+    const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
+    hipError_t e = first && last ? launch_dphase<false, kPhDeriv | kPhScatter>(ph[i].n, g, a, q, s)
+                   : first       ? launch_dphase<false, kPhDeriv>(ph[i].n, g, a, q, s)
+                   : last        ? launch_dphase<false, kPhScatter>(ph[i].n, g, a, q, s)
+                                 : launch_dphase<false, 0>(ph[i].n, g, a, q, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a, hipStream_t s) {
   const dim3 grid = grid_for(a.shard_bytes, kc.nv, a.n_stripes);
   if (kc.variant == Variant::kRegister) {
@@ -1949,8 +2076,7 @@ static hipError_t launch_decode_one(const KernelChoice &kc, const DecodeArgs &a,
     RS_MAT_NV(5) RS_MAT_NV(6) RS_MAT_NV(7) RS_MAT_NV(8)
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(k_decode_generic<1>, grid, dim3(kBlock), 0, s, a);
-  return hipGetLastError();
+  return launch_decode_generic(a, s);
 }
 
 hipError_t launch_pattern_plan(const uint8_t *d_present, uint64_t present_stride, uint32_t k, uint32_t m, uint32_t C,

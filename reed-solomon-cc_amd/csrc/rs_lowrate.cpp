@@ -13,7 +13,7 @@
 //  * reconstruct (rs_gf.hpp scalar_reconstruct_low): the erasure-locator decode of
 //    root.zig:268-335 in the low-rate position layout (recovery at [C, C + m), [C + m, W)
 //    erased), on the decode kernels with the FFT truncated to k (k_decode_reg for
-//    W <= 32, k_decode_generic otherwise) — no host solve, any (k, m) useHighRate accepts.
+//    W <= 32, launch_decode_generic otherwise) — no host solve, any (k, m) useHighRate accepts.
 //  * small codes: a bit-sliced network of the encode map (<= 64 outputs) and of each
 //    erasure pattern's reconstruct map (<= 64 restored, by GF(2) linear algebra on the
 //    host), HBM-bound; the FFT-form kernels run until such a network is compiled.
@@ -324,7 +324,7 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
     HIP_TRY(launch_decode(kc, a, s));
     return RS_OK;
   }
-  return in_scratch_slices(n, static_cast<uint64_t>(p->W) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
+  return in_scratch_slices(n, decode_generic_rows(p->W, p->trunc, k) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
     DecodeArgs b = a;
     b.orig += s0 * ostride;
     b.rec += s0 * rstride;

@@ -1,0 +1,223 @@
+"""Dataflow model of the generic reconstruct's launch sequence (rs_kernels.hip
+launch_decode_generic / k_dphase): the phase schedule (xform_phases), the sub-problem ->
+positions map, the IFFT's zero tail (positions past round_up(trunc, span) neither written
+nor read), the formal derivative split into in-register bits and partner loads, the FFT's
+kept rows (Y) and skipped sub-problems, and the scatter — against the layer-by-layer
+decode of root.zig:268-335 (Generic.zig:15-147 transforms, root.zig:306-312 derivative).
+
+Symbols are 64-bit vectors over GF(2) and every twiddle a fixed GF(2)-linear map keyed by
+(transform, layer distance, group start), so a schedule that skips, reorders or drops a
+butterfly, or reads a position the previous phase did not write, changes the result. CPU
+only: it checks index logic, not field arithmetic (the GPU parity tests do that)."""
+import random
+
+import pytest
+
+MASK = (1 << 64) - 1
+
+
+def rotl(x, a):
+    a %= 64
+    return ((x << a) | (x >> (64 - a))) & MASK if a else x
+
+
+def tw(key):
+    h = hash(key) & 0xFFFFFFFF
+    a, b = 1 + h % 61, 1 + (h >> 8) % 59
+    return lambda y: rotl(y, a) ^ rotl(y, b) ^ (y >> (h % 7 + 1))
+
+
+def ifft_bf(x, i, j, f):
+    x[j] ^= x[i]
+    x[i] ^= f(x[j])
+
+
+def fft_bf(x, i, j, f):
+    x[i] ^= f(x[j])
+    x[j] ^= x[i]
+
+
+def ifft_ref(x, size, trunc):
+    d = 1
+    while 4 * d <= size:
+        for r in range(0, min(trunc, size), 4 * d):
+            m01, m23, m02 = tw(("i", d, r, 0)), tw(("i", d, r, 2)), tw(("i", d, r, 1))
+            for i in range(r, r + d):
+                ifft_bf(x, i, i + d, m01)
+                ifft_bf(x, i + 2 * d, i + 3 * d, m23)
+                ifft_bf(x, i, i + 2 * d, m02)
+                ifft_bf(x, i + d, i + 3 * d, m02)
+        d *= 4
+    if d < size:  # final odd layer, distance size / 2, no truncation
+        t = tw(("i", d, 0, 9))
+        for i in range(d):
+            ifft_bf(x, i, i + d, t)
+
+
+def fft_ref(x, size, trunc):
+    lg = size.bit_length() - 1
+    d = 1 << (lg - 2) if lg >= 2 else 0
+    d4 = size
+    while d >= 1 and 4 * d == d4:
+        for r in range(0, min(trunc, size), 4 * d):
+            m01, m23, m02 = tw(("f", d, r, 0)), tw(("f", d, r, 2)), tw(("f", d, r, 1))
+            for i in range(r, r + d):
+                fft_bf(x, i, i + 2 * d, m02)
+                fft_bf(x, i + d, i + 3 * d, m02)
+                fft_bf(x, i, i + d, m01)
+                fft_bf(x, i + 2 * d, i + 3 * d, m23)
+        d4 = d
+        d //= 4
+    if d4 == 2:  # radix-2 tail, distance 1
+        for r in range(0, min(trunc, size), 2):
+            fft_bf(x, r, r + 1, tw(("f", 1, r, 9)))
+
+
+def deriv_ref(x, W):
+    for i in range(1, W):  # root.zig:306-312
+        w = i & -i
+        for j in range(w):
+            x[i - w + j] ^= x[i + j]
+
+
+def decode_ref(src, W, trunc, trunc_fft, dst):
+    x = [src.get(p, 0) for p in range(W)]
+    ifft_ref(x, W, trunc)
+    deriv_ref(x, W)
+    fft_ref(x, W, trunc_fft)
+    return {p: x[p] for p in dst if p < trunc_fft}
+
+
+# ---- the launch sequence, as rs_kernels.hip writes it
+def xform_phases(size, inv):
+    lg = size.bit_length() - 1
+    n4, layer, r2_done, out = lg // 2, 0, not (lg & 1), []
+    while True:
+        c = min(3, n4 - layer)
+        with_r2 = (not r2_done) and layer + c == n4 and c < 3
+        nn = (1 << (2 * c)) << (1 if with_r2 else 0)
+        dlo_log = 2 * layer if inv else (0 if (with_r2 or c == 0) else lg - 2 * (layer + c))
+        out.append((nn, dlo_log))
+        layer += c
+        r2_done = r2_done or with_r2 or c == 0
+        if not (layer < n4 or not r2_done):
+            return out
+
+
+def round_up(x, a):
+    return (x + a - 1) // a * a
+
+
+def ifft_sub(v, N, size, rmax, blk, dlo_log):
+    jd, jd4 = 1, 4
+    while jd4 <= N:
+        d = jd << dlo_log
+        for jr in range(0, N, jd4):
+            r = blk + (jr << dlo_log)
+            if r < rmax:
+                m01, m23, m02 = tw(("i", d, r, 0)), tw(("i", d, r, 2)), tw(("i", d, r, 1))
+                for i in range(jr, jr + jd):
+                    ifft_bf(v, i, i + jd, m01)
+                    ifft_bf(v, i + 2 * jd, i + 3 * jd, m23)
+                    ifft_bf(v, i, i + 2 * jd, m02)
+                    ifft_bf(v, i + jd, i + 3 * jd, m02)
+        jd, jd4 = jd4, jd4 * 4
+    if jd < N:
+        t = tw(("i", jd << dlo_log, 0, 9))
+        for i in range(jd):
+            ifft_bf(v, i, jd + i, t)
+
+
+def fft_sub(v, N, size, rmax, blk, dlo_log):
+    jd4, jd = N, N >> 2
+    while jd != 0:
+        d = jd << dlo_log
+        for jr in range(0, N, jd4):
+            r = blk + (jr << dlo_log)
+            if r < rmax:
+                m01, m23, m02 = tw(("f", d, r, 0)), tw(("f", d, r, 2)), tw(("f", d, r, 1))
+                for i in range(jr, jr + jd):
+                    fft_bf(v, i, i + 2 * jd, m02)
+                    fft_bf(v, i + jd, i + 3 * jd, m02)
+                    fft_bf(v, i, i + jd, m01)
+                    fft_bf(v, i + 2 * jd, i + 3 * jd, m23)
+        jd4, jd = jd, jd >> 2
+    if jd4 == 2:
+        for jr in range(0, N, 2):
+            r = blk + jr
+            if r < rmax:
+                fft_bf(v, jr, jr + 1, tw(("f", 1, r, 9)))
+
+
+def decode_phased(src, W, trunc, trunc_fft, dst):
+    ri, rf = min(trunc, W), min(trunc_fft, W)
+    fph = xform_phases(W, False)
+    ylen = min(W, round_up(rf, 1 << fph[0][1])) if len(fph) > 1 else 0
+    X = [None] * W  # None: never written (reading it is a schedule bug)
+    Y = [None] * max(ylen, 1)
+    out = {}
+    lim = 0
+    for i, (N, dl) in enumerate(xform_phases(W, True)):
+        span = N << dl
+        wl = round_up(ri, span)
+        n_src = ri if i == 0 else lim
+        for sub in range(wl // N):
+            blk, lo = (sub >> dl) * span, sub & ((1 << dl) - 1)
+            ps = [blk + lo + (j << dl) for j in range(N)]
+            if i == 0:
+                v = [src.get(p, 0) if p < n_src else 0 for p in ps]
+            else:
+                v = [X[p] if p < n_src else 0 for p in ps]
+            ifft_sub(v, N, W, ri, blk, dl)
+            for j, p in enumerate(ps):
+                if p < wl:
+                    X[p] = v[j]
+        lim = wl
+    for i, (N, dl) in enumerate(fph):
+        span = N << dl
+        wl = round_up(rf, span)
+        first, last = i == 0, i + 1 == len(fph)
+        snap = list(Y)
+        for sub in range(wl // N):
+            blk, lo = (sub >> dl) * span, sub & ((1 << dl) - 1)
+            ps = [blk + lo + (j << dl) for j in range(N)]
+            if first:
+                v = [X[p] for p in ps]
+                for j in range(N):  # in-register derivative bits (ascending)
+                    bb = 1
+                    while bb < N:
+                        if not j & bb:
+                            v[j] ^= v[j + bb]
+                        bb <<= 1
+                for b in range(dl):  # partner loads (X is not written in this phase)
+                    if (lo >> b) & 1:
+                        continue
+                    for j in range(N):
+                        v[j] ^= X[blk + lo + (1 << b) + (j << dl)]
+            else:
+                v = [snap[p] for p in ps]
+            fft_sub(v, N, W, rf, blk, dl)
+            for j, p in enumerate(ps):
+                if last:
+                    if p < rf and p in dst:
+                        out[p] = v[j]
+                elif p < ylen:
+                    Y[p] = v[j]
+    assert all(x is not None for x in X)
+    return out
+
+
+def case(W, trunc, trunc_fft, seed):
+    rng = random.Random(seed)
+    src = {p: rng.getrandbits(64) for p in range(trunc) if rng.random() < 0.7}
+    dst = {p for p in range(trunc_fft) if rng.random() < 0.3}
+    return src, dst
+
+
+@pytest.mark.parametrize("W,trunc,trunc_fft", [
+    (64, 40, 40), (128, 100, 70), (256, 200, 77), (512, 300, 300), (1024, 1000, 33),
+    (2048, 1512, 300), (2048, 1128, 1128), (4096, 2600, 2600), (8192, 5024, 1000), (128, 128, 128),
+])
+def test_phased_decode_matches_layer_walk(W, trunc, trunc_fft):
+    src, dst = case(W, trunc, trunc_fft, W * 7 + trunc)
+    assert decode_phased(src, W, trunc, trunc_fft, dst) == decode_ref(src, W, trunc, trunc_fft, dst)
