@@ -52,10 +52,18 @@ typedef u32 v4 __attribute__((ext_vector_type(4)));
     x[j] = MUX(a, b << d, m);        \
     x[j + d] = MUX(a >> d, b, m);    \
   }
+// the transpose masks in VGPRs when RS_VMASK (a v_bitop3 with an SGPR source issues at ~2/3
+// rate with two or more waves per SIMD, profiles/r04/valu_probe2.log; VOP3 takes no literal)
+#if RS_VMASK
+#define KMASK(c) ({ u32 m_ = (c); asm("" : "+v"(m_)); m_; })
+#else
+#define KMASK(c) (c)
+#endif
 __device__ __forceinline__ void tr8(u32 *x) {
-  TRS(0, 4, 0x0F0F0F0Fu) TRS(1, 4, 0x0F0F0F0Fu) TRS(2, 4, 0x0F0F0F0Fu) TRS(3, 4, 0x0F0F0F0Fu)
-  TRS(0, 2, 0x33333333u) TRS(1, 2, 0x33333333u) TRS(4, 2, 0x33333333u) TRS(5, 2, 0x33333333u)
-  TRS(0, 1, 0x55555555u) TRS(2, 1, 0x55555555u) TRS(4, 1, 0x55555555u) TRS(6, 1, 0x55555555u)
+  const u32 f = KMASK(0x0F0F0F0Fu), t = KMASK(0x33333333u), s = KMASK(0x55555555u);
+  TRS(0, 4, f) TRS(1, 4, f) TRS(2, 4, f) TRS(3, 4, f)
+  TRS(0, 2, t) TRS(1, 2, t) TRS(4, 2, t) TRS(5, 2, t)
+  TRS(0, 1, s) TRS(2, 1, s) TRS(4, 1, s) TRS(6, 1, s)
 }
 #if RS_NT & 1
 #define LDV(p) __builtin_nontemporal_load((const v4 *)(p))
@@ -247,7 +255,7 @@ void emit_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::v
 //   RS_AMD_NET_SHARED    0: the classic form instead of the shared-input form
 //   RS_AMD_NET_BALANCE   0: one wave per 8-output tile in the shared form
 struct Tuning {
-  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, balance = 1;
+  int prefetch = 0, waves = 0, nt = 3, barrier = -1, units = 1, tile = 8, shared = -1, balance = 1, vmask = 1;
 };
 
 int env_int(const char *name, int def) {
@@ -260,11 +268,12 @@ Tuning tuning() {
   t.tile = env_int("RS_AMD_NET_TILE", t.tile) >= 8 ? 8 : 4;
   t.shared = env_int("RS_AMD_NET_SHARED", t.shared);
   t.balance = env_int("RS_AMD_NET_BALANCE", t.balance) != 0;
+  t.vmask = env_int("RS_AMD_NET_VMASK", t.vmask) != 0;
   return t;
 }
 
 std::string tuning_key(const Tuning &t) {
-  return "t" + std::to_string(t.tile) + "s" + std::to_string(t.shared) + (t.balance ? "" : "nb");
+  return "t" + std::to_string(t.tile) + "s" + std::to_string(t.shared) + (t.balance ? "" : "nb") + (t.vmask ? "" : "nv");
 }
 
 // Shared-input form (generate_shared): one workgroup of n_tiles waves per 4 KiB unit,
@@ -295,7 +304,8 @@ uint32_t kernel_tiles(const Tuning &t, const NetSpec &spec) {
 
 }  // namespace
 
-const char *net_prelude() { return kPrelude; }
+bool net_vmask() { return env_int("RS_AMD_NET_VMASK", 1) != 0; }
+std::string net_prelude() { return std::string("#define RS_VMASK ") + (net_vmask() ? "1\n" : "0\n") + kPrelude; }
 void emit_network_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::vector<bool> &init, int t) {
   emit_input(o, rows, init, t);
 }
@@ -340,7 +350,7 @@ std::string generate_shared(const NetSpec &spec, const std::string &name, const 
   const uint32_t mult = 1;
   const uint32_t BW = T * mult, nb = (n_in + BW - 1) / BW;
   std::ostringstream o;
-  o << "#define RS_NT " << tu.nt << "\n" << kPrelude;
+  o << "#define RS_NT " << tu.nt << "\n#define RS_VMASK " << tu.vmask << "\n" << kPrelude;
   o << "extern \"C\" __global__ __launch_bounds__(" << 64 * T << ") ";
   if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";
   o << "void " << name
@@ -435,7 +445,7 @@ std::string generate_with(const NetSpec &spec, const std::string &name, const Tu
   // evict early) cost 10-15 % there, so by default they are kept for 1-tile maps only
   const int nt = n_tiles == 1 ? tu.nt : (tu.nt & 2);
   const uint32_t P = spec.pieces;  // stripes per wave unit (1, or 2 / 4 for 2 / 1 KiB shards)
-  o << "#define RS_NT " << nt << "\n" << kPrelude;
+  o << "#define RS_NT " << nt << "\n#define RS_VMASK " << tu.vmask << "\n" << kPrelude;
   if (P > 1) o << kPreludeSmall;
   o << "extern \"C\" __global__ __launch_bounds__(256) ";
   if (tu.waves) o << "__attribute__((amdgpu_waves_per_eu(" << tu.waves << ", 8))) ";

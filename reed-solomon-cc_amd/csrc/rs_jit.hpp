@@ -71,7 +71,8 @@ std::string generate(const NetSpec &spec, const std::string &name);
 // st over a wave's 4 KiB unit; RS_NT must be defined first), and one input's
 // Four-Russians XOR network into accumulators a<r> (rows[r] = 16-bit mask of the
 // input planes feeding accumulator r; `init`: accumulators already assigned).
-const char *net_prelude();
+std::string net_prelude();  // RS_AMD_NET_VMASK (default 1): transpose masks in VGPRs
+bool net_vmask();
 void emit_network_input(std::ostringstream &o, const std::vector<uint16_t> &rows, std::vector<bool> &init, int t);
 
 struct Kernel {

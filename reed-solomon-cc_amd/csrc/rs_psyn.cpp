@@ -29,7 +29,7 @@ bool skip_erased() { return true; }
 
 std::string key_of(const Spec &s) {
   std::string k = "psyn2:p" + std::to_string(prefetch()) + "w" + std::to_string(waves()) + "s" +
-                  std::to_string(skip_erased()) + ":" + std::to_string(s.k) +
+                  std::to_string(skip_erased()) + "v" + std::to_string(jit::net_vmask()) + ":" + std::to_string(s.k) +
                   ":" + std::to_string(s.m) + ":" + std::to_string(s.flags) + ":";
   k.append(reinterpret_cast<const char *>(s.images.data()), s.images.size() * sizeof(uint16_t));
   k.append(reinterpret_cast<const char *>(s.cantor.data()), s.cantor.size() * sizeof(uint16_t));
@@ -331,7 +331,7 @@ std::string generate_solve(const uint16_t *cantor, const std::string &name) {
 
 const jit::Kernel *get_solve(const uint16_t *cantor, std::string &err) {
   // v3: output groups (blockIdx.z), one alpha chain per syndrome
-  std::string key = "psolve:v3:o" + std::to_string(kSolveMaxOut) + ":";
+  std::string key = "psolve:v3:o" + std::to_string(kSolveMaxOut) + "v" + std::to_string(jit::net_vmask()) + ":";
   key.append(reinterpret_cast<const char *>(cantor), 16 * sizeof(uint16_t));
   uint64_t h = 1469598103934665603ull;
   for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
