@@ -377,7 +377,7 @@ int rs_reconstruct_batch_dev(uint64_t k, uint64_t m, size_t sb, uint64_t n_strip
     }
     // launch_decode_generic: the transform plus the FFT's kept rows, per stripe
     const uint64_t rows = decode_generic_rows(plan->work, a.trunc, a.trunc_fft);
-    const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, scratch_cap() / (rows * sb)));
+    const uint64_t per = slice_stripes(n_stripes, rows * sb);
     void *scratch = nullptr;
     HIP_TRY(dev_malloc_async(&scratch, per * rows * sb, s));
     for (uint64_t s0 = 0; s0 < n_stripes; s0 += per) {

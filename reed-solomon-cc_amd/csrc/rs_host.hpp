@@ -234,11 +234,18 @@ int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out
 // HBM for the life of the process; *off_fft = byte offset of the FFT tables
 int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &out, size_t &off_fft);
 
-constexpr uint64_t kScratchCap = 1ull << 30;  // generic path: scratch per launch
+constexpr uint64_t kScratchCap = 2ull << 30;  // generic path: scratch per launch
 // the generic kernels' scratch cap per launch: kScratchCap, or RS_AMD_SCRATCH_CAP_MB
 inline uint64_t scratch_cap() {
   const char *e = std::getenv("RS_AMD_SCRATCH_CAP_MB");
   return e && *e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20 : kScratchCap;
+}
+// stripes per scratch slice: as many as fit the cap, spread evenly over the slices (a short
+// last slice runs its launches at lower occupancy)
+inline uint64_t slice_stripes(uint64_t n, uint64_t per_stripe_bytes) {
+  const uint64_t fit = std::max<uint64_t>(1, std::min<uint64_t>(n, scratch_cap() / per_stripe_bytes));
+  const uint64_t slices = (n + fit - 1) / fit;
+  return (n + slices - 1) / slices;
 }
 
 // ------------------------------------------------- kernel selection (rs_select.cpp)

@@ -723,6 +723,10 @@ struct XformIO {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const uint8_t *row) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(row), static_cast<short>(0), 0x7FFFFFFF, 0x00020000);
 }
+// a resource with no records: loads through it read zero, stores through it are dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t zero_rsrc() {
+  return __builtin_amdgcn_make_buffer_rsrc(nullptr, static_cast<short>(0), 0, 0x00020000);
+}
 template <int NV>
 __device__ __forceinline__ void ldb(Sym<NV> &s, __amdgpu_buffer_rsrc_t r, uint32_t off) {
   static_assert(NV == 1, "generic column walk: one dword pair per lane");
@@ -860,22 +864,28 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
 // ---- the generic reconstruct as a launch sequence (launch_decode_generic): one launch per
 // phase of xform_ph, the phase's sub-problems across the grid (y), so a small batch still
 // fills the chip. Grid: x = column units, y = sub-problem, z = stripes (strided).
-// Per stripe the scratch holds X (W positions: the IFFT, in place) and Y (the positions the
-// truncated FFT still needs, decode_generic_rows). The steps ride on the phases:
+// Per stripe the scratch holds X (W positions: the IFFT, in place), A and B (the positions
+// the truncated FFT still needs after its first phase; decode_generic_rows). The steps ride
+// on the phases:
 //  * GATHER (first IFFT phase): positions come from the received shards * pre, zero where
 //    nothing was received (root.zig:291-303), instead of a staging pass;
 //  * the IFFT writes only positions < round_up(trunc, span): a sub-problem past the
 //    truncation is all zero and so is what it would write (the next phase reads zeros);
-//  * DERIV (first FFT phase, X -> Y): the formal derivative (root.zig:306-312) as
-//    out[p] = in[p] ^ XOR over clear bits b of p of in[p + 2^b] (every read an original
-//    value: a sum of shifted copies of X). The phase spans every position, so bits the
-//    sub-problem holds combine in VGPRs (ascending, reads above writes); the low bits
-//    (b < dlo_log) are partner loads from X, which this phase does not write;
+//  * the formal derivative (root.zig:306-312) is out[p] = in[p] ^ XOR over clear bits b of
+//    p of in[p + 2^b] (every read an original value): D = I + H + L, H the bits the first
+//    FFT phase F1 holds (it spans every position), L the bits below its stride. L acts on
+//    the low bits only and F1 on the high bits only (its twiddles depend on the group, not
+//    on the low bits), so F1 D = F1 (I + H) + L F1. DERIV (first FFT phase): H in VGPRs
+//    (ascending, reads above writes), A = F1((I + H) X); SPLITB: the same sub-problem
+//    again without H, B = F1(X); LSUM (second FFT phase): A + L B, L's bits the
+//    sub-problem holds in VGPRs, the ones below its stride as loads of B (none for
+//    W = 2048). No partner loads of X (tests/test_decode_phases_model.py checks this
+//    against the layer-by-layer decode);
 //  * the FFT writes only positions < round_up(trunc_fft, span) and skips sub-problems past
 //    the truncation (their outputs feed nothing: root.zig:318 reads [0, trunc));
 //  * SCATTER (last FFT phase): only the erased positions, * post, into the restored rows
 //    (root.zig:320-326).
-enum : int { kPhGather = 1, kPhDeriv = 2, kPhScatter = 4 };
+enum : int { kPhGather = 1, kPhDeriv = 2, kPhScatter = 4, kPhSplitB = 8, kPhLsum = 16 };
 
 struct PhaseArgs {
   const uint8_t *src;  // stripe s's input: src + s * src_stride, position p at + p * sb
@@ -884,31 +894,78 @@ struct PhaseArgs {
   uint64_t sb, size, rmax, ti;
   const RsTab *tabs;
   uint32_t dlo_log;
+  const uint8_t *src2;  // LSUM: B (stride src_stride)
+  uint8_t *dst2;        // SPLITB: B (stride dst_stride)
 };
 
 template <int N, bool INV, int MODE>
 __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
-  uint32_t off;
-  if (!lane_offset<1>(q.sb, false, off)) return;
+  // lanes past the shard's last chunk stay (the lane reads below need every lane): they
+  // load at offset 0 and store nothing
+  uint32_t off = 0;
+  const bool act = lane_offset<1>(q.sb, false, off);
+  if (!act) off = 0;
   const uint64_t sb = q.sb, sub = blockIdx.y, dlo = 1ull << q.dlo_log;
   const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
   for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
     Sym<1> v[N];
     if constexpr ((MODE & kPhGather) != 0) {
-      const uint8_t *orig = a.orig + s * a.orig_stripe_stride + off;
-      const uint8_t *rec = a.rec + s * a.rec_stripe_stride + off;
+      // the sub-problem's sources in one vector load (lane j: position j), then per position
+      // a lane read and a load through a buffer resource with no records when nothing was
+      // received (reads zero): no scalar load, wait and branch in front of every load
+      const uint8_t *orig = a.orig + s * a.orig_stripe_stride;
+      const uint8_t *rec = a.rec + s * a.rec_stripe_stride;
       const RsTab *tab_pre = a.tab_pre + s * a.pattern_stride;
       const int32_t *pos_src = a.pos_src + s * a.pattern_stride;
+      const uint32_t ln = __lane_id();
+      const uint64_t lp = blk + lo + (static_cast<uint64_t>(ln) << q.dlo_log);
+      const int32_t my = ln < static_cast<uint32_t>(N) && lp < q.n_src ? pos_src[lp] : -1;
+      int32_t srcs[N];
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        srcs[j] = __builtin_amdgcn_readlane(my, j);
+        const uint8_t *row = ((srcs[j] & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(srcs[j] & kSrcIndexMask) * sb;
+        ldb(v[j], srcs[j] >= 0 ? row_rsrc(row) : zero_rsrc(), off);
+      }
+#pragma unroll
+      for (int j = 0; j < N; j++)
+        if (srcs[j] >= 0) dev::mul_inplace(v[j], dev::load_tab(tab_pre + blk + lo + (static_cast<uint64_t>(j) << q.dlo_log)));
+    } else if constexpr ((MODE & kPhLsum) != 0) {
+      const uint8_t *A = q.src + s * q.src_stride, *B = q.src2 + s * q.src_stride;
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        const int32_t src = p < q.n_src ? ((const __attribute__((address_space(4))) int32_t *)pos_src)[p] : -1;
-        if (src >= 0) {
-          const uint8_t *base = (src & kSrcRecovery) ? rec : orig;
-          dev::load_sym(v[j], base + static_cast<uint64_t>(src & kSrcIndexMask) * sb, 0u, false);
-          dev::mul_inplace(v[j], dev::load_tab(tab_pre + p));
-        } else {
-          dev::zero(v[j]);
+        if (p < q.n_src) ldb(v[j], row_rsrc(B + p * sb), off);
+        else dev::zero(v[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < N; j++) {  // L's bits in VGPRs: v[j] = XOR over clear bits of B[j + bb]
+        Sym<1> t;
+        dev::zero(t);
+#pragma unroll
+        for (int bb = 1; bb < N; bb <<= 1)
+          if (!(j & bb)) dev::xor_into(t, v[j + bb]);
+        v[j] = t;
+      }
+      for (uint32_t b = 0; b < q.dlo_log; b++) {  // L's bits below the stride: loads of B
+        if ((lo >> b) & 1) continue;                // wave-uniform
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+          const uint64_t p = blk + lo + (1ull << b) + (static_cast<uint64_t>(j) << q.dlo_log);
+          if (p < q.n_src) {
+            Sym<1> t;
+            ldb(t, row_rsrc(B + p * sb), off);
+            dev::xor_into(v[j], t);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p < q.n_src) {
+          Sym<1> t;
+          ldb(t, row_rsrc(A + p * sb), off);
+          dev::xor_into(v[j], t);
         }
       }
     } else {
@@ -919,21 +976,12 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
         if (p < q.n_src) ldb(v[j], row_rsrc(x + p * sb), off);
         else dev::zero(v[j]);
       }
-      if constexpr ((MODE & kPhDeriv) != 0) {
+      if constexpr ((MODE & kPhDeriv) != 0) {  // H: the bits this sub-problem holds
 #pragma unroll
         for (int j = 0; j < N; j++)
 #pragma unroll
           for (int bb = 1; bb < N; bb <<= 1)
             if (!(j & bb)) dev::xor_into(v[j], v[j + bb]);
-        for (uint32_t b = 0; b < q.dlo_log; b++) {
-          if ((lo >> b) & 1) continue;  // wave-uniform
-#pragma unroll
-          for (int j = 0; j < N; j++) {
-            Sym<1> t;
-            ldb(t, row_rsrc(x + (blk + lo + (1ull << b) + (static_cast<uint64_t>(j) << q.dlo_log)) * sb), off);
-            dev::xor_into(v[j], t);
-          }
-        }
       }
     }
     if constexpr (INV) ifft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
@@ -942,14 +990,15 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
       uint8_t *out = a.out + s * a.out_stripe_stride;
       const RsTab *tab_post = a.tab_post + s * a.pattern_stride;
       const int32_t *pos_dst = a.pos_dst + s * a.pattern_stride;
+      const uint32_t ln = __lane_id();
+      const uint64_t lp = blk + lo + (static_cast<uint64_t>(ln) << q.dlo_log);
+      const int32_t my = ln < static_cast<uint32_t>(N) && lp < q.rmax ? pos_dst[lp] : -1;
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p >= q.rmax) continue;
-        const int32_t dst = ((const __attribute__((address_space(4))) int32_t *)pos_dst)[p];
+        const int32_t dst = __builtin_amdgcn_readlane(my, j);
         if (dst >= 0) {
-          dev::mul_inplace(v[j], dev::load_tab(tab_post + p));
-          dev::store_sym(out + static_cast<uint64_t>(dst) * sb, off, v[j], false);
+          dev::mul_inplace(v[j], dev::load_tab(tab_post + blk + lo + (static_cast<uint64_t>(j) << q.dlo_log)));
+          if (act) stb(row_rsrc(out + static_cast<uint64_t>(dst) * sb), off, v[j]);
         }
       }
     } else {
@@ -957,7 +1006,23 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p < q.n_dst) stb(row_rsrc(y + p * sb), off, v[j]);
+        if (act && p < q.n_dst) stb(row_rsrc(y + p * sb), off, v[j]);
+      }
+    }
+    if constexpr ((MODE & kPhSplitB) != 0) {  // B = F1(X): the sub-problem again, without H
+      const uint8_t *x = q.src + s * q.src_stride;
+      uint8_t *y = q.dst2 + s * q.dst_stride;
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p < q.n_src) ldb(v[j], row_rsrc(x + p * sb), off);
+        else dev::zero(v[j]);
+      }
+      fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (act && p < q.n_dst) stb(row_rsrc(y + p * sb), off, v[j]);
       }
     }
   }
@@ -1991,25 +2056,30 @@ static void xform_phases(uint64_t size, bool inv, std::vector<XPhase> &out) {
 
 static uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
-// positions of the FFT's Y buffer: those the phases after the first read (0 for one phase)
+// positions of the FFT's A and B buffers: those the phases after the first read (0 for one phase)
 static uint64_t decode_y_rows(uint64_t W, uint64_t rmax_fft) {
   std::vector<XPhase> ph;
   xform_phases(W, false, ph);
   return ph.size() > 1 ? std::min(W, round_up(rmax_fft, 1ull << ph[0].dlo_log)) : 0;
 }
 
-uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft) {
-  return W + decode_y_rows(W, trunc_fft ? trunc_fft : trunc);
+uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft) {  // X | A | B
+  return W + 2 * decode_y_rows(W, trunc_fft ? trunc_fft : trunc);
 }
 
 template <bool INV, int MODE>
 static hipError_t launch_dphase(uint32_t n, dim3 g, const DecodeArgs &a, const PhaseArgs &q, hipStream_t s) {
-  switch (n) {
+  if constexpr ((MODE & (kPhGather | kPhDeriv)) != 0) {  // first phases: 64 points for every W >= 64
+    if (n != 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_dphase<64, INV, MODE>), g, dim3(kBlock), 0, s, a, q);
+  } else {
+    switch (n) {
 #define RS_DPH_CASE(N_) \
   case N_: hipLaunchKernelGGL((k_dphase<N_, INV, MODE>), g, dim3(kBlock), 0, s, a, q); break;
-    RS_DPH_CASE(2) RS_DPH_CASE(4) RS_DPH_CASE(8) RS_DPH_CASE(16) RS_DPH_CASE(32) RS_DPH_CASE(64)
+      RS_DPH_CASE(2) RS_DPH_CASE(4) RS_DPH_CASE(8) RS_DPH_CASE(16) RS_DPH_CASE(32) RS_DPH_CASE(64)
 #undef RS_DPH_CASE
-    default: return hipErrorInvalidValue;
+      default: return hipErrorInvalidValue;
+    }
   }
   return hipGetLastError();
 }
@@ -2020,8 +2090,8 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   const uint64_t W = a.work, sb = a.shard_bytes;
   if (W < 2 || (W & (W - 1)) || W > 65536 || sb % 64) return hipErrorInvalidValue;
   const uint64_t ri = std::min<uint64_t>(a.trunc, W), rf = std::min<uint64_t>(a.trunc_fft ? a.trunc_fft : a.trunc, W);
-  const uint64_t ylen = decode_y_rows(W, rf), stride = (W + ylen) * sb;
-  uint8_t *X = a.scratch, *Y = a.scratch + W * sb;
+  const uint64_t ylen = decode_y_rows(W, rf), stride = (W + 2 * ylen) * sb;
+  uint8_t *X = a.scratch, *Y = a.scratch + W * sb, *B = Y + ylen * sb;
   const dim3 g0 = grid_for(sb, 1, 1);
   const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
   std::vector<XPhase> ph;
@@ -2029,7 +2099,8 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   uint64_t lim = 0;  // positions the previous IFFT phase wrote (the rest are zero)
   for (size_t i = 0; i < ph.size(); i++) {
     const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(ri, span);
-    PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[i].ti, a.tab_ifft, ph[i].dlo_log};
+    PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[i].ti, a.tab_ifft, ph[i].dlo_log, nullptr,
+                nullptr};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
     hipError_t e = i == 0 ? launch_dphase<true, kPhGather>(ph[i].n, g, a, q, s)
                           : launch_dphase<true, 0>(ph[i].n, g, a, q, s);
@@ -2041,10 +2112,12 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
     const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(rf, span);
     const bool first = i == 0, last = i + 1 == ph.size();
     PhaseArgs q{first ? X : Y, Y, stride, stride, first ? W : ylen, ylen, sb, W, rf, ph[i].ti, a.tab_fft,
-                ph[i].dlo_log};
+                ph[i].dlo_log, B, B};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
     hipError_t e = first && last ? launch_dphase<false, kPhDeriv | kPhScatter>(ph[i].n, g, a, q, s)
-                   : first       ? launch_dphase<false, kPhDeriv>(ph[i].n, g, a, q, s)
+                   : first       ? launch_dphase<false, kPhDeriv | kPhSplitB>(ph[i].n, g, a, q, s)
+                   : i == 1      ? (last ? launch_dphase<false, kPhLsum | kPhScatter>(ph[i].n, g, a, q, s)
+                                         : launch_dphase<false, kPhLsum>(ph[i].n, g, a, q, s))
                    : last        ? launch_dphase<false, kPhScatter>(ph[i].n, g, a, q, s)
                                  : launch_dphase<false, 0>(ph[i].n, g, a, q, s);
     if (e != hipSuccess) return e;

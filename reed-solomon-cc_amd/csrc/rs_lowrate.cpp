@@ -227,7 +227,7 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
 // generic kernels walk a scratch of `per_stripe` positions x sb per stripe, in slices
 template <class F>
 int in_scratch_slices(uint64_t n, uint64_t per_stripe_bytes, hipStream_t s, F &&launch) {
-  const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(n, scratch_cap() / per_stripe_bytes));
+  const uint64_t per = slice_stripes(n, per_stripe_bytes);
   void *scratch = nullptr;
   HIP_TRY(dev_malloc_async(&scratch, per * per_stripe_bytes, s));
   hipError_t e = hipSuccess;

@@ -518,7 +518,7 @@ int rs_reconstruct_batch_dev_patterns(uint64_t k, uint64_t m, size_t sb, uint64_
     } else {
       // launch_decode_generic: the transform plus the FFT's kept rows, per stripe
       const uint64_t rows = decode_generic_rows(W, a.trunc, a.trunc_fft);
-      const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(n_stripes, scratch_cap() / (rows * sb)));
+      const uint64_t cap = slice_stripes(n_stripes, rows * sb);
       void *scratch = nullptr;
       e = dev_malloc_async(&scratch, cap * rows * sb, s);
       for (uint64_t s0 = 0; e == hipSuccess && s0 < n_stripes; s0 += cap) {

@@ -154,7 +154,8 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
     fph = xform_phases(W, False)
     ylen = min(W, round_up(rf, 1 << fph[0][1])) if len(fph) > 1 else 0
     X = [None] * W  # None: never written (reading it is a schedule bug)
-    Y = [None] * max(ylen, 1)
+    Y = [None] * max(ylen, 1)  # A: F1((I + H) X), then the later phases in place
+    B = [None] * max(ylen, 1)  # F1(X)
     out = {}
     lim = 0
     for i, (N, dl) in enumerate(xform_phases(W, True)):
@@ -173,6 +174,10 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
                 if p < wl:
                     X[p] = v[j]
         lim = wl
+    # the derivative D = I + H + L (H: the bits the first FFT phase holds, L: the bits below
+    # its stride). L acts on the low bits only and the first phase F1 on the high bits only,
+    # so F1 D = F1 (I + H) + L F1: the first phase writes A = F1((I + H) X) and B = F1(X),
+    # the second reads A + L B (L's bits it holds in registers, the rest as loads of B)
     for i, (N, dl) in enumerate(fph):
         span = N << dl
         wl = round_up(rf, span)
@@ -189,11 +194,30 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
                         if not j & bb:
                             v[j] ^= v[j + bb]
                         bb <<= 1
-                for b in range(dl):  # partner loads (X is not written in this phase)
+                if not last:  # B = F1(X): the same sub-problem without the derivative
+                    w = [X[p] for p in ps]
+                    fft_sub(w, N, W, rf, blk, dl)
+                    for j, p in enumerate(ps):
+                        if p < ylen:
+                            B[p] = w[j]
+            elif i == 1:
+                lsum = fph[0][1]  # L's bits: below the first phase's stride
+                v = [B[p] for p in ps]
+                for j in range(N):  # L's bits this sub-problem holds (ascending, t excludes v[j])
+                    t, bb = 0, 1
+                    while bb < N:
+                        if not j & bb:
+                            t ^= v[j + bb]
+                        bb <<= 1
+                    v[j] = t
+                for b in range(dl):  # L's bits below this phase's stride: loads of B
                     if (lo >> b) & 1:
                         continue
                     for j in range(N):
-                        v[j] ^= X[blk + lo + (1 << b) + (j << dl)]
+                        v[j] ^= B[blk + lo + (1 << b) + (j << dl)]
+                assert (N << dl) == (1 << lsum) or blk > 0
+                for j, p in enumerate(ps):
+                    v[j] ^= snap[p]
             else:
                 v = [snap[p] for p in ps]
             fft_sub(v, N, W, rf, blk, dl)
