@@ -312,6 +312,7 @@ const jit::Kernel *wps_solve_kernel(WpsSlot &ws);
 int fdec_mode();
 bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags);
 // RS_AMD_PDEC (default on): a reused wide-code pattern gets its pattern-compiled fused kernel
+constexpr uint64_t kPdecMaxK = 256;  // pattern-compiled fused reconstruct: codes up to k = 256
 bool pdec_enabled();
 // exp, log, log_walsh in HBM (384 KiB per device)
 int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw);

@@ -286,8 +286,10 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   // the background compile for good.
   // a reused wide-code pattern gets the fused kernel with the pattern compiled in (constant
   // locator multiplies: no scalar-loaded masks); it replaces the syndrome
-  // path's e x e network, and a direct network (few losses) stays ahead of it
-  const bool pdec_on = e > 0 && !every_lost && m <= 64 && pdec_enabled() && fdec_supports(k, m, sb, flags) &&
+  // path's e x e network, and a direct network (few losses) stays ahead of it. k <= 256: the
+  // compile grows with the code (RS(200,55) 8-16 s, RS(1000,64) 45 s of hipRTC per pattern)
+  const bool pdec_on = e > 0 && !every_lost && m <= 64 && k <= kPdecMaxK && pdec_enabled() &&
+                       fdec_supports(k, m, sb, flags) &&
                        (mode == "auto" || mode == "net");
   const bool syn_wins = !pdec_on && syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
   if (lite && !full && !use_net && !use_net_async && !syn_wins && !pdec_on) {

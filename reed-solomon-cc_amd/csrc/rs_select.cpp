@@ -178,7 +178,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
       (mode == "auto" || mode == "net")) {
     const bool syn = syndrome_pick(k, m, e, flags_none(), sb, mode);
     const bool direct = decode_kind(k, m, flags_none(), e, have, sb) != 0 && direct_net_async(e, k, sb, mode, k, m, flags_none());
-    if (!direct && pdec_enabled()) return net_name("fft_pdecode", k, m);  // steady state: the pattern compiled in
+    if (!direct && k <= kPdecMaxK && pdec_enabled()) return net_name("fft_pdecode", k, m);  // steady state: the pattern compiled in
     if (fdec_mode() == 1 || !(direct || (syn && 4 * e >= 3 * m && jit::enabled() &&
                                          jit::supports_async(static_cast<uint32_t>(e), static_cast<uint32_t>(e), sb))))
       return net_name("fft_decode", k, m);

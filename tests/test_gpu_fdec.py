@@ -38,6 +38,8 @@ def fdec(monkeypatch):
 
 # chunk 16 / 32 / 64, one to sixteen data blocks, last block partial or full
 FDEC_KM = [(200, 55), (33, 17), (64, 64), (100, 20), (16, 16), (30, 9), (128, 32), (1000, 64), (65, 33)]
+# pattern-compiled kernels (k <= 256): one hipRTC compile per pattern, 1-16 s each
+PDEC_KM = [(200, 55), (33, 17), (100, 20), (16, 16), (65, 33)]
 
 
 @pytest.mark.parametrize("k,m", FDEC_KM)
@@ -57,7 +59,7 @@ def test_fdec_random_patterns(oracle, fdec, k, m):
         assert (got == data[:, present[:k] == 0]).all(), (k, m, sorted(lost))
 
 
-@pytest.mark.parametrize("k,m", FDEC_KM)
+@pytest.mark.parametrize("k,m", PDEC_KM)
 def test_pdec_pattern_compiled(oracle, monkeypatch, k, m):
     """The fused reconstruct with the pattern compiled in (fftnet::Spec::present: constant
     locator multiplies, static rows / blocks / outputs, pruned butterflies), reached through
