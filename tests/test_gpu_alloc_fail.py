@@ -56,18 +56,25 @@ def test_every_allocation_fails_cleanly(k, m, sb, lost):
     n = R.debug_fail_alloc(-1)
     assert n >= 4, n
     assert R.debug_release_caches() == 0
-    free0 = free_bytes()
-    ooms = 0
-    for i in range(n):
-        R.debug_fail_alloc(i)
-        try:
-            cycle(k, m, sb, lost)
-        except R.OutOfMemory:  # noqa: F821 (generated from the Zig error set)
-            ooms += 1
-        finally:
-            R.debug_fail_alloc(-1)
-        R.net_wait()
-        assert R.debug_release_caches() == 0, i
-        assert free_bytes() == free0, (i, free0 - free_bytes())
-    assert ooms >= 1
+
+    def walk(check):
+        free0, ooms = free_bytes(), 0
+        for i in range(n):
+            R.debug_fail_alloc(i)
+            try:
+                cycle(k, m, sb, lost)
+            except R.OutOfMemory:  # noqa: F821 (generated from the Zig error set)
+                ooms += 1
+            finally:
+                R.debug_fail_alloc(-1)
+            R.net_wait()
+            assert R.debug_release_caches() == 0, i
+            if check:
+                assert free_bytes() == free0, (i, free0 - free_bytes())
+        return ooms
+
+    # the first walk may take one-time runtime allocations (a fallback kernel's first
+    # launch, its scratch); the second must leave the device exactly as it found it
+    walk(False)
+    assert walk(True) >= 1
     cycle(k, m, sb, lost)  # and the library still works
