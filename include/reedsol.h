@@ -194,17 +194,19 @@ const char *rs_reconstruct_kernel_name(uint64_t original_count, uint64_t recover
  * built on the GPU), "fft_syndromes+psyn_solve" (chunk 16 / 32 / 64 otherwise: FFT syndromes
  * with per-stripe masks + the e x e solve in output groups of 8), "pattern_matrix"
  * (per-stripe e x k table matrices, W <= 32, max_e <= 8) or "pattern_fft" (the reference's
- * decode on the generic FFT kernels: D1, D2-dropping codes, everything else). These are
+ * decode on the generic FFT kernels: D1, D2-dropping codes, everything else) or
+ * "pattern_fft_low" (low-rate codes: the same decode in the low-rate layout). These are
  * what a call is planned to run; rs_last_kernels reports what it did run. */
 const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes,
                                     uint32_t max_e, uint32_t flags);
 
-/* Large reconstruct network maps (the e x e syndrome map of wide codes, e.g. RS(200,55)
- * losing 55 data shards: ~16-36 s of hipRTC) compile in a background thread. A wide-code
- * pattern's first calls run the fused FFT reconstruct (rs_fft_decode_*, the pattern as
- * data); where a network beats it, the pattern's second call queues the full plan's build
- * and, behind it, the network's compile on the background worker, and the calls run the
- * fused kernel until the network is loaded. rs_net_wait blocks until the worker is idle
+/* Per-pattern kernels of wide codes compile in a background thread. A wide-code pattern's
+ * first calls run the fused FFT reconstruct with the pattern as data (rs_fft_decode_*,
+ * nothing compiled per pattern); its second call queues the full plan's build and, behind
+ * it, the compile of its steady-state kernel on the background worker: the fused kernel
+ * with the pattern compiled in (rs_fft_pdecode_*, k <= 256; RS(200,55): 8-16 s of hipRTC),
+ * or a network where one beats it (few losses: the direct map; RS_AMD_FDEC=0: the e x e
+ * syndrome map), and the calls run the first form until it is loaded. rs_net_wait blocks until the worker is idle
  * (no plan build or compile queued or running): after two calls + rs_net_wait the next
  * call runs the pattern's steady-state kernel. RS_AMD_JIT_SYNC=1 compiles in the calling
  * thread instead. Returns RS_OK. */
