@@ -896,16 +896,37 @@ struct PhaseArgs {
   uint32_t dlo_log;
   const uint8_t *src2;  // LSUM: B (stride src_stride)
   uint8_t *dst2;        // SPLITB: B (stride dst_stride)
+  bool contig;          // shard rows in the contiguous lane layout (shard_bytes % 512 == 0)
 };
+
+// scratch rows (X, A, B): lane u's 4 symbols as one 8-byte (lo, hi) pair at u * 8, so a
+// wave's access is 512 contiguous bytes (one dwordx2 per lane); only the shard rows keep the
+// reference's chunk layout (Generic.zig:152-156)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void ldp(Sym<1> &s, __amdgpu_buffer_rsrc_t r, uint32_t o) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0);
+  s.l[0] = v.x;
+  s.h[0] = v.y;
+}
+__device__ __forceinline__ void stp(__amdgpu_buffer_rsrc_t r, uint32_t o, const Sym<1> &s) {
+  u32x2 v;
+  v.x = s.l[0];
+  v.y = s.h[0];
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, o, 0, 0);
+}
 
 template <int N, bool INV, int MODE>
 __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
-  // lanes past the shard's last chunk stay (the lane reads below need every lane): they
-  // load at offset 0 and store nothing
-  uint32_t off = 0;
-  const bool act = lane_offset<1>(q.sb, false, off);
-  if (!act) off = 0;
-  const uint64_t sb = q.sb, sub = blockIdx.y, dlo = 1ull << q.dlo_log;
+  // lane unit u (4 symbols of one shard column); lanes past the shard's last unit stay (the
+  // lane reads below need every lane): they load at offset 0 and store nothing
+  const uint64_t sb = q.sb, u = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const bool act = u < sb / 8;
+  const uint32_t so = act ? static_cast<uint32_t>(u * 8) : 0u;  // scratch offset
+  // shard-row offset: the contiguous lane layout (512-B waves, lo / hi halves paired by a
+  // lane swap) where the shard is whole 512-B waves, else 4 + 4 bytes of one 64-B chunk
+  const uint32_t io = act ? dev::lane_byte_offset<1>(u / 64, static_cast<uint32_t>(u % 64), q.contig) : 0u;
+  const uint32_t io_h = io + (q.contig ? 256u : 32u);
+  const uint64_t sub = blockIdx.y, dlo = 1ull << q.dlo_log;
   const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
   for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
     Sym<1> v[N];
@@ -925,8 +946,13 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
       for (int j = 0; j < N; j++) {
         srcs[j] = __builtin_amdgcn_readlane(my, j);
         const uint8_t *row = ((srcs[j] & kSrcRecovery) ? rec : orig) + static_cast<uint64_t>(srcs[j] & kSrcIndexMask) * sb;
-        ldb(v[j], srcs[j] >= 0 ? row_rsrc(row) : zero_rsrc(), off);
+        const __amdgpu_buffer_rsrc_t r = srcs[j] >= 0 ? row_rsrc(row) : zero_rsrc();
+        v[j].l[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io, 0, 0);
+        v[j].h[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io_h, 0, 0);
       }
+      if (q.contig)  // pair after every load is issued (a swap behind its own load waits for it)
+#pragma unroll
+        for (int j = 0; j < N; j++) dev::pair_halves(v[j], true);
 #pragma unroll
       for (int j = 0; j < N; j++)
         if (srcs[j] >= 0) dev::mul_inplace(v[j], dev::load_tab(tab_pre + blk + lo + (static_cast<uint64_t>(j) << q.dlo_log)));
@@ -935,7 +961,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p < q.n_src) ldb(v[j], row_rsrc(B + p * sb), off);
+        if (p < q.n_src) ldp(v[j], row_rsrc(B + p * sb), so);
         else dev::zero(v[j]);
       }
 #pragma unroll
@@ -954,7 +980,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
           const uint64_t p = blk + lo + (1ull << b) + (static_cast<uint64_t>(j) << q.dlo_log);
           if (p < q.n_src) {
             Sym<1> t;
-            ldb(t, row_rsrc(B + p * sb), off);
+            ldp(t, row_rsrc(B + p * sb), so);
             dev::xor_into(v[j], t);
           }
         }
@@ -964,7 +990,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
         if (p < q.n_src) {
           Sym<1> t;
-          ldb(t, row_rsrc(A + p * sb), off);
+          ldp(t, row_rsrc(A + p * sb), so);
           dev::xor_into(v[j], t);
         }
       }
@@ -973,7 +999,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p < q.n_src) ldb(v[j], row_rsrc(x + p * sb), off);
+        if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
         else dev::zero(v[j]);
       }
       if constexpr ((MODE & kPhDeriv) != 0) {  // H: the bits this sub-problem holds
@@ -996,9 +1022,12 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const int32_t dst = __builtin_amdgcn_readlane(my, j);
-        if (dst >= 0) {
+        if (dst >= 0) {  // wave-uniform
           dev::mul_inplace(v[j], dev::load_tab(tab_post + blk + lo + (static_cast<uint64_t>(j) << q.dlo_log)));
-          if (act) stb(row_rsrc(out + static_cast<uint64_t>(dst) * sb), off, v[j]);
+          if (q.contig) dev::pair_halves(v[j], true);  // back to the lo / hi halves (an involution)
+          const __amdgpu_buffer_rsrc_t r = act ? row_rsrc(out + static_cast<uint64_t>(dst) * sb) : zero_rsrc();
+          __builtin_amdgcn_raw_buffer_store_b32(v[j].l[0], r, io, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(v[j].h[0], r, io_h, 0, 0);
         }
       }
     } else {
@@ -1006,7 +1035,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (act && p < q.n_dst) stb(row_rsrc(y + p * sb), off, v[j]);
+        if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
       }
     }
     if constexpr ((MODE & kPhSplitB) != 0) {  // B = F1(X): the sub-problem again, without H
@@ -1015,14 +1044,14 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p < q.n_src) ldb(v[j], row_rsrc(x + p * sb), off);
+        if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
         else dev::zero(v[j]);
       }
       fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (act && p < q.n_dst) stb(row_rsrc(y + p * sb), off, v[j]);
+        if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
       }
     }
   }
@@ -2092,6 +2121,7 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   const uint64_t ri = std::min<uint64_t>(a.trunc, W), rf = std::min<uint64_t>(a.trunc_fft ? a.trunc_fft : a.trunc, W);
   const uint64_t ylen = decode_y_rows(W, rf), stride = (W + 2 * ylen) * sb;
   uint8_t *X = a.scratch, *Y = a.scratch + W * sb, *B = Y + ylen * sb;
+  const bool contig = contig_ok(sb, 1);
   const dim3 g0 = grid_for(sb, 1, 1);
   const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
   std::vector<XPhase> ph;
@@ -2100,7 +2130,7 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   for (size_t i = 0; i < ph.size(); i++) {
     const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(ri, span);
     PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[i].ti, a.tab_ifft, ph[i].dlo_log, nullptr,
-                nullptr};
+                nullptr, contig};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
     hipError_t e = i == 0 ? launch_dphase<true, kPhGather>(ph[i].n, g, a, q, s)
                           : launch_dphase<true, 0>(ph[i].n, g, a, q, s);
@@ -2112,7 +2142,7 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
     const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(rf, span);
     const bool first = i == 0, last = i + 1 == ph.size();
     PhaseArgs q{first ? X : Y, Y, stride, stride, first ? W : ylen, ylen, sb, W, rf, ph[i].ti, a.tab_fft,
-                ph[i].dlo_log, B, B};
+                ph[i].dlo_log, B, B, contig};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
     hipError_t e = first && last ? launch_dphase<false, kPhDeriv | kPhScatter>(ph[i].n, g, a, q, s)
                    : first       ? launch_dphase<false, kPhDeriv | kPhSplitB>(ph[i].n, g, a, q, s)
