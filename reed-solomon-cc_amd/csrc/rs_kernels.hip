@@ -897,7 +897,31 @@ struct PhaseArgs {
   const uint8_t *src2;  // LSUM: B (stride src_stride)
   uint8_t *dst2;        // SPLITB: B (stride dst_stride)
   bool contig;          // shard rows in the contiguous lane layout (shard_bytes % 512 == 0)
+  // NI > 0 (the first FFT phase): the IFFT's last phase runs on the loaded rows first
+  const RsTab *tabs_i;
+  uint64_t ti_i, rmax_i;
+  uint32_t dlo_i;
 };
+
+// The IFFT's last phase inside the first FFT phase's sub-problem: that sub-problem (fixed
+// position bits below dlo_f, registers j over the bits above) is the union of G = N / NI of
+// the IFFT phase's sub-problems (bits below dlo_i = dlo_f + log2 G fixed): group g holds
+// registers g + t G, t < NI (tests/test_decode_phases_model.py)
+template <int N, int NI>
+__device__ __forceinline__ void ifft_last_in(Sym<1> *v, const PhaseArgs &q) {
+  if constexpr (NI > 0) {
+    constexpr int G = N / NI;
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      Sym<1> w[NI];
+#pragma unroll
+      for (int t = 0; t < NI; t++) w[t] = v[g + t * G];
+      ifft_sub<NI, 1>(w, q.tabs_i, q.ti_i, q.size, q.rmax_i, 0, q.dlo_i);
+#pragma unroll
+      for (int t = 0; t < NI; t++) v[g + t * G] = w[t];
+    }
+  }
+}
 
 // scratch rows (X, A, B): lane u's 4 symbols as one 8-byte (lo, hi) pair at u * 8, so a
 // wave's access is 512 contiguous bytes (one dwordx2 per lane); only the shard rows keep the
@@ -915,7 +939,7 @@ __device__ __forceinline__ void stp(__amdgpu_buffer_rsrc_t r, uint32_t o, const 
   __builtin_amdgcn_raw_buffer_store_b64(v, r, o, 0, 0);
 }
 
-template <int N, bool INV, int MODE>
+template <int N, bool INV, int MODE, int NI = 0>
 __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
   // lane unit u (4 symbols of one shard column); lanes past the shard's last unit stay (the
   // lane reads below need every lane): they load at offset 0 and store nothing
@@ -1002,6 +1026,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
         if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
         else dev::zero(v[j]);
       }
+      ifft_last_in<N, NI>(v, q);
       if constexpr ((MODE & kPhDeriv) != 0) {  // H: the bits this sub-problem holds
 #pragma unroll
         for (int j = 0; j < N; j++)
@@ -1047,6 +1072,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
         if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
         else dev::zero(v[j]);
       }
+      ifft_last_in<N, NI>(v, q);
       fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
 #pragma unroll
       for (int j = 0; j < N; j++) {
@@ -2113,6 +2139,19 @@ static hipError_t launch_dphase(uint32_t n, dim3 g, const DecodeArgs &a, const P
   return hipGetLastError();
 }
 
+// the first FFT phase with the IFFT's last phase fused in (64-point sub-problems)
+static hipError_t launch_dphase_fused(uint32_t ni, dim3 g, const DecodeArgs &a, const PhaseArgs &q, hipStream_t s) {
+  constexpr int M = kPhDeriv | kPhSplitB;
+  switch (ni) {
+#define RS_DPF_CASE(NI_) \
+  case NI_: hipLaunchKernelGGL((k_dphase<64, false, M, NI_>), g, dim3(kBlock), 0, s, a, q); break;
+    RS_DPF_CASE(2) RS_DPF_CASE(4) RS_DPF_CASE(8) RS_DPF_CASE(16) RS_DPF_CASE(32) RS_DPF_CASE(64)
+#undef RS_DPF_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 // Decoder.decode (root.zig:268-335) over any W as one launch per transform phase
 // (a.scratch: decode_generic_rows positions per stripe)
 static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
@@ -2124,16 +2163,22 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   const bool contig = contig_ok(sb, 1);
   const dim3 g0 = grid_for(sb, 1, 1);
   const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
-  std::vector<XPhase> ph;
-  xform_phases(W, true, ph);
+  std::vector<XPhase> ph, iph;
+  xform_phases(W, true, iph);
+  // with two or more IFFT phases the last one runs inside the first FFT phase's loads (its
+  // sub-problems are the union of G of the IFFT phase's): one pass over X less, and X read
+  // before it is the previous phase's output
+  const bool fuse = iph.size() >= 2;
+  const size_t n_ifft = fuse ? iph.size() - 1 : iph.size();
   uint64_t lim = 0;  // positions the previous IFFT phase wrote (the rest are zero)
-  for (size_t i = 0; i < ph.size(); i++) {
-    const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(ri, span);
-    PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[i].ti, a.tab_ifft, ph[i].dlo_log, nullptr,
-                nullptr, contig};
-    const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
-    hipError_t e = i == 0 ? launch_dphase<true, kPhGather>(ph[i].n, g, a, q, s)
-                          : launch_dphase<true, 0>(ph[i].n, g, a, q, s);
+  for (size_t i = 0; i < n_ifft; i++) {
+    ph.assign(1, iph[i]);
+    const uint64_t span = static_cast<uint64_t>(ph[0].n) << ph[0].dlo_log, wl = round_up(ri, span);
+    PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[0].ti, a.tab_ifft, ph[0].dlo_log, nullptr,
+                nullptr, contig, nullptr, 0, 0, 0};
+    const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[0].n), gz);
+    hipError_t e = i == 0 ? launch_dphase<true, kPhGather>(ph[0].n, g, a, q, s)
+                          : launch_dphase<true, 0>(ph[0].n, g, a, q, s);
     if (e != hipSuccess) return e;
     lim = wl;
   }
@@ -2141,10 +2186,13 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   for (size_t i = 0; i < ph.size(); i++) {
     const uint64_t span = static_cast<uint64_t>(ph[i].n) << ph[i].dlo_log, wl = round_up(rf, span);
     const bool first = i == 0, last = i + 1 == ph.size();
-    PhaseArgs q{first ? X : Y, Y, stride, stride, first ? W : ylen, ylen, sb, W, rf, ph[i].ti, a.tab_fft,
-                ph[i].dlo_log, B, B, contig};
+    PhaseArgs q{first ? X : Y, Y, stride, stride, first ? (fuse ? lim : W) : ylen, ylen, sb, W, rf, ph[i].ti, a.tab_fft,
+                ph[i].dlo_log, B, B, contig, a.tab_ifft, iph.back().ti, ri, iph.back().dlo_log};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
+    if (first && fuse && (ph[i].n != 64 || last || (64u >> (iph.back().dlo_log - ph[i].dlo_log)) != iph.back().n))
+      return hipErrorInvalidValue;  // the shapes xform_phases gives every W >= 128
     hipError_t e = first && last ? launch_dphase<false, kPhDeriv | kPhScatter>(ph[i].n, g, a, q, s)
+                   : first && fuse ? launch_dphase_fused(iph.back().n, g, a, q, s)
                    : first       ? launch_dphase<false, kPhDeriv | kPhSplitB>(ph[i].n, g, a, q, s)
                    : i == 1      ? (last ? launch_dphase<false, kPhLsum | kPhScatter>(ph[i].n, g, a, q, s)
                                          : launch_dphase<false, kPhLsum>(ph[i].n, g, a, q, s))

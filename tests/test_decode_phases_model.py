@@ -158,7 +158,10 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
     B = [None] * max(ylen, 1)  # F1(X)
     out = {}
     lim = 0
-    for i, (N, dl) in enumerate(xform_phases(W, True)):
+    iph = xform_phases(W, True)
+    fuse = len(iph) >= 2  # the last IFFT phase runs inside the first FFT phase's loads
+    NI, DI = iph[-1]
+    for i, (N, dl) in enumerate(iph[:-1] if fuse else iph):
         span = N << dl
         wl = round_up(ri, span)
         n_src = ri if i == 0 else lim
@@ -186,8 +189,21 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
         for sub in range(wl // N):
             blk, lo = (sub >> dl) * span, sub & ((1 << dl) - 1)
             ps = [blk + lo + (j << dl) for j in range(N)]
+
+            def load_x():
+                if not fuse:
+                    return [X[p] for p in ps]
+                x = [X[p] if p < lim else 0 for p in ps]
+                G = N // NI
+                assert blk == 0 and (1 << (DI - dl)) == G
+                for g in range(G):  # the IFFT's last phase on each of its sub-problems
+                    w = [x[g + t * G] for t in range(NI)]
+                    ifft_sub(w, NI, W, ri, 0, DI)
+                    for t in range(NI):
+                        x[g + t * G] = w[t]
+                return x
             if first:
-                v = [X[p] for p in ps]
+                v = load_x()
                 for j in range(N):  # in-register derivative bits (ascending)
                     bb = 1
                     while bb < N:
@@ -195,7 +211,7 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
                             v[j] ^= v[j + bb]
                         bb <<= 1
                 if not last:  # B = F1(X): the same sub-problem without the derivative
-                    w = [X[p] for p in ps]
+                    w = load_x()
                     fft_sub(w, N, W, rf, blk, dl)
                     for j, p in enumerate(ps):
                         if p < ylen:
@@ -227,7 +243,6 @@ def decode_phased(src, W, trunc, trunc_fft, dst):
                         out[p] = v[j]
                 elif p < ylen:
                     Y[p] = v[j]
-    assert all(x is not None for x in X)
     return out
 
 
