@@ -2122,19 +2122,23 @@ uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft) {  
   return W + 2 * decode_y_rows(W, trunc_fft ? trunc_fft : trunc);
 }
 
-template <bool INV, int MODE>
+// NS: the sub-problem sizes a mode runs with for W = 64 .. 65536 (xform_phases): the first
+// phases and the middle ones are 64 points, only the last phases vary (instantiating just
+// those keeps the build time down)
+template <bool INV, int MODE, int NS>
 static hipError_t launch_dphase(uint32_t n, dim3 g, const DecodeArgs &a, const PhaseArgs &q, hipStream_t s) {
-  if constexpr ((MODE & (kPhGather | kPhDeriv)) != 0) {  // first phases: 64 points for every W >= 64
-    if (n != 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((k_dphase<64, INV, MODE>), g, dim3(kBlock), 0, s, a, q);
-  } else {
-    switch (n) {
-#define RS_DPH_CASE(N_) \
-  case N_: hipLaunchKernelGGL((k_dphase<N_, INV, MODE>), g, dim3(kBlock), 0, s, a, q); break;
-      RS_DPH_CASE(2) RS_DPH_CASE(4) RS_DPH_CASE(8) RS_DPH_CASE(16) RS_DPH_CASE(32) RS_DPH_CASE(64)
-#undef RS_DPH_CASE
-      default: return hipErrorInvalidValue;
+  switch (n) {
+#define RS_DPH_CASE(N_)                                                              \
+  case N_:                                                                           \
+    if constexpr ((NS & N_) != 0) {                                                  \
+      hipLaunchKernelGGL((k_dphase<N_, INV, MODE>), g, dim3(kBlock), 0, s, a, q);    \
+      break;                                                                         \
+    } else {                                                                         \
+      return hipErrorInvalidValue;                                                   \
     }
+    RS_DPH_CASE(2) RS_DPH_CASE(4) RS_DPH_CASE(8) RS_DPH_CASE(16) RS_DPH_CASE(32) RS_DPH_CASE(64)
+#undef RS_DPH_CASE
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -2177,8 +2181,8 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
     PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, W, ri, ph[0].ti, a.tab_ifft, ph[0].dlo_log, nullptr,
                 nullptr, contig, nullptr, 0, 0, 0};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[0].n), gz);
-    hipError_t e = i == 0 ? launch_dphase<true, kPhGather>(ph[0].n, g, a, q, s)
-                          : launch_dphase<true, 0>(ph[0].n, g, a, q, s);
+    hipError_t e = i == 0 ? launch_dphase<true, kPhGather, 64>(ph[0].n, g, a, q, s)
+                          : launch_dphase<true, 0, 64>(ph[0].n, g, a, q, s);
     if (e != hipSuccess) return e;
     lim = wl;
   }
@@ -2191,13 +2195,13 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
     const dim3 g(g0.x, static_cast<uint32_t>(wl / ph[i].n), gz);
     if (first && fuse && (ph[i].n != 64 || last || (64u >> (iph.back().dlo_log - ph[i].dlo_log)) != iph.back().n))
       return hipErrorInvalidValue;  // the shapes xform_phases gives every W >= 128
-    hipError_t e = first && last ? launch_dphase<false, kPhDeriv | kPhScatter>(ph[i].n, g, a, q, s)
-                   : first && fuse ? launch_dphase_fused(iph.back().n, g, a, q, s)
-                   : first       ? launch_dphase<false, kPhDeriv | kPhSplitB>(ph[i].n, g, a, q, s)
-                   : i == 1      ? (last ? launch_dphase<false, kPhLsum | kPhScatter>(ph[i].n, g, a, q, s)
-                                         : launch_dphase<false, kPhLsum>(ph[i].n, g, a, q, s))
-                   : last        ? launch_dphase<false, kPhScatter>(ph[i].n, g, a, q, s)
-                                 : launch_dphase<false, 0>(ph[i].n, g, a, q, s);
+    // first: W = 64 (one phase each way) or fused with the IFFT's last phase (W >= 128)
+    hipError_t e = first && last ? launch_dphase<false, kPhDeriv | kPhScatter, 64>(ph[i].n, g, a, q, s)
+                   : first       ? (fuse ? launch_dphase_fused(iph.back().n, g, a, q, s) : hipErrorInvalidValue)
+                   : i == 1      ? (last ? launch_dphase<false, kPhLsum | kPhScatter, 126>(ph[i].n, g, a, q, s)
+                                         : launch_dphase<false, kPhLsum, 64>(ph[i].n, g, a, q, s))
+                   : last        ? launch_dphase<false, kPhScatter, 30>(ph[i].n, g, a, q, s)
+                                 : hipErrorInvalidValue;  // no fourth FFT phase below W = 2^19
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
