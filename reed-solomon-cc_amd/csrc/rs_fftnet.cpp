@@ -319,26 +319,11 @@ __device__ __forceinline__ void rmul(u32 *x, cptr M, const Km KM) {
   u32 s[8], o[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) s[j] = SWN(x[j]);
-#ifdef RS_RMUL_VLOAD
-  // masks through vector loads (a laundered zero VGPR offset keeps them off the scalar
-  // path): in-order vmcnt lets the compiler keep several planes' masks in flight
-  u32 vz = 0;
-  asm volatile("" : "+v"(vz));
-  const v4 *M4 = (const v4 *)(const void *)M + vz;
-#endif
 #pragma unroll
   for (int i0 = 0; i0 < 8; i0 += RS_RMUL_G) {
     u32 m[16 * RS_RMUL_G];
-#ifdef RS_RMUL_VLOAD
-#pragma unroll
-    for (int t = 0; t < 4 * RS_RMUL_G; t++) {
-      const v4 q = M4[4 * i0 + t];
-      m[4 * t] = q[0]; m[4 * t + 1] = q[1]; m[4 * t + 2] = q[2]; m[4 * t + 3] = q[3];
-    }
-#else
 #pragma unroll
     for (int t = 0; t < 16 * RS_RMUL_G; t++) m[t] = M[16 * i0 + t];
-#endif
 #pragma unroll
     for (int g = 0; g < RS_RMUL_G; g++) {
       u32 a = x[0] & m[16 * g];
@@ -388,15 +373,12 @@ unsigned long long *stamp_buffer(int dev) {
 // the transpose / basis masks in VGPRs (RS_AMD_FFT_VMASK, default on)
 int vmask_of() { return env_int("RS_AMD_FFT_VMASK", 1) ? 1 : 0; }
 
-// s_setprio alternation between the SIMD-pair halves every n butterflies (0: off)
-int prio_of() { return std::max(0, env_int("RS_AMD_FFT_PRIO", 0)); }
-
-// runtime-multiply masks through vector loads (RS_AMD_FFT_RMULV=1) instead of scalar loads
-int rmul_vload() { return env_int("RS_AMD_FFT_RMULV", 0) ? 1 : 0; }
-
-// runtime-multiply output planes per scalar-load step (RS_AMD_FFT_RMULG: 1, 2, 4, 8)
+// runtime-multiply output planes per scalar-load step (RS_AMD_FFT_RMULG: 1, 2, 4, 8). 4: per-stripe
+// RS(200,55) max_e 55 7.35 -> 6.66 ms, RS(16,16) 2.79 -> 2.71 ms (profiles/r04/patterns/rmul_ab.log).
+// Measured and removed: the masks through vector loads (7.35 -> 8.9 ms), s_setprio turns
+// between the SIMD-pair halves (c4 neutral to 8 % slower, profiles/r04/prio1.log)
 int rmul_group() {
-  const int g = env_int("RS_AMD_FFT_RMULG", 1);
+  const int g = env_int("RS_AMD_FFT_RMULG", 4);
   return g == 2 || g == 4 || g == 8 ? g : 1;
 }
 
@@ -543,22 +525,12 @@ struct Gen {
 
   int sched = 0;  // sched_barrier every `sched` butterflies (bounds the scheduler's interleaving)
   int nbf = 0;
-  // SIMD-pair arbitration (RS_AMD_FFT_PRIO = n): waves w and w + 4 share a SIMD and the
-  // younger loses VALU arbitration to the older (MI355X_MICROARCH.md, two waves per SIMD),
-  // so in a phase of equal work it finishes last and every barrier waits for it. Every n
-  // butterflies the two halves swap s_setprio, so they take turns.
-  int prio = 0, nprio = 0, pturn = 0;
 
   // one butterfly on named 8-dword positions with zero tracking
   void butterfly(const std::string &xn, bool &zx, const std::string &yn, bool &zy, bool inv, const Tw &t) {
     const auto X = regs(xn), Y = regs(yn);
     if (zx && zy) return;
     if (sched && ++nbf % sched == 0) o << "  __builtin_amdgcn_sched_barrier(0);\n";
-    if (prio && ++nprio % prio == 0) {
-      pturn ^= 1;
-      o << "  if (w & 4u) __builtin_amdgcn_s_setprio(" << pturn << "); else __builtin_amdgcn_s_setprio(" << (pturn ^ 1)
-        << ");\n";
-    }
     if (t.zero && st) st->xor_only++;
     if (inv) {  // ifftPartial, Generic.zig:171-192: y ^= x; x ^= M y
       if (!zx) {
@@ -638,7 +610,6 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   Gen g;
   g.st = stats;
   g.sched = sched_of();  // sched_barrier per butterfly: bounds the scheduler's interleaving (compile time)
-  g.prio = prio_of();
   Stats dummy;
   if (!g.st) g.st = &dummy;
   std::ostringstream &o = g.o;
@@ -685,7 +656,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   }
   o << "#define RS_AUX_LD 2\n#define RS_AUX_ST 2\n#define RS_STAMPS " << ((dbg & 64) ? 1 : 0) << "\n"
     << (s.decode && (dbg & 8) ? "#define RS_DBG_NORMUL 1\n" : "")
-    << "#define RS_RMUL_G " << rmul_group() << "\n" << (rmul_vload() ? "#define RS_RMUL_VLOAD 1\n" : "") << kPrelude;
+    << "#define RS_RMUL_G " << rmul_group() << "\n" << kPrelude;
   // 1 KiB shards (pieces 2): a unit's two 1 KiB halves are the same slice of stripes
   // 2u and 2u + 1 (resources R* and R*1; the second is the zero-record RZ past the
   // batch, so its loads read zeros and its stores are dropped)
@@ -1477,8 +1448,7 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft4:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":d" +
-                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":v" + std::to_string(rmul_vload()) +
-                  ":r" + std::to_string(prio_of()) + ":k" + std::to_string(vmask_of()) + ":" +
+                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":k" + std::to_string(vmask_of()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
