@@ -1083,6 +1083,81 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
   }
 }
 
+// ---- the low-rate generic encode as one launch per transform phase (launch_encode_low_phases):
+// coefficients = IFFT_C(originals at [0, k), trunc k) in region 0 of the stripe's scratch
+// (the first phase gathers the original rows); recovery chunk j = FFT_C(coefficients, skew
+// (j+1)C, trunc t_j = min(C, m - jC)) in region 1 + (j - chunk0), its last phase storing
+// the recovery rows jC + p directly. The IFFT's last phase runs inside the first FFT
+// phase's loads (as launch_decode_generic does), so region 0 is read, never rewritten, by
+// every chunk. Grid y = (chunk of the launch, sub-problem) for the FFT phases.
+enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4 };
+
+template <int N, int MODE, int NI>
+__global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, uint32_t subs, uint32_t from_chunk) {
+  const uint64_t sb = q.sb, u = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const bool act = u < sb / 8;
+  const uint32_t so = act ? static_cast<uint32_t>(u * 8) : 0u;
+  const uint32_t io = act ? dev::lane_byte_offset<1>(u / 64, static_cast<uint32_t>(u % 64), q.contig) : 0u;
+  const uint32_t io_h = io + (q.contig ? 256u : 32u);
+  constexpr bool kFft = (MODE & kEpFft) != 0;
+  const uint64_t C = q.size, dlo = 1ull << q.dlo_log;
+  const uint32_t ch = kFft ? blockIdx.y / subs : 0u;  // chunk of this launch
+  const uint64_t sub = kFft ? blockIdx.y % subs : blockIdx.y;
+  const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
+  const uint64_t j = a.chunk0 + ch;  // recovery chunk
+  const uint64_t rmax = kFft ? (a.m - j * C < C ? a.m - j * C : C) : q.rmax;
+  if (kFft && blk >= rmax) return;  // wave-uniform: outputs past the chunk's truncation feed nothing
+  const RsTab *tabs = kFft ? q.tabs + j * a.tabs_per_chunk : q.tabs;
+  const uint64_t n_dst = kFft ? (rmax + dlo - 1) / dlo * dlo : q.n_dst;  // what later phases read
+  for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    Sym<1> v[N];
+    const uint8_t *x = q.src + s * q.src_stride + (from_chunk ? (1 + ch) * C * sb : 0);
+    if constexpr ((MODE & kEpGather) != 0) {
+      const uint8_t *d = a.data + s * a.data_stripe_stride;
+#pragma unroll
+      for (int jj = 0; jj < N; jj++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
+        const __amdgpu_buffer_rsrc_t r = p < q.n_src ? row_rsrc(d + p * sb) : zero_rsrc();
+        v[jj].l[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io, 0, 0);
+        v[jj].h[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io_h, 0, 0);
+      }
+      if (q.contig)
+#pragma unroll
+        for (int jj = 0; jj < N; jj++) dev::pair_halves(v[jj], true);
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < N; jj++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
+        if (p < q.n_src) ldp(v[jj], row_rsrc(x + p * sb), so);
+        else dev::zero(v[jj]);
+      }
+      ifft_last_in<N, NI>(v, q);
+    }
+    if constexpr (kFft) fft_sub<N, 1>(v, tabs, q.ti, C, rmax, blk, q.dlo_log);
+    else ifft_sub<N, 1>(v, tabs, q.ti, C, rmax, blk, q.dlo_log);
+    if constexpr ((MODE & kEpOut) != 0) {
+      uint8_t *par = a.parity + s * a.parity_stripe_stride + j * C * sb;
+#pragma unroll
+      for (int jj = 0; jj < N; jj++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
+        if (p < rmax) {  // wave-uniform
+          if (q.contig) dev::pair_halves(v[jj], true);
+          const __amdgpu_buffer_rsrc_t r = act ? row_rsrc(par + p * sb) : zero_rsrc();
+          __builtin_amdgcn_raw_buffer_store_b32(v[jj].l[0], r, io, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(v[jj].h[0], r, io_h, 0, 0);
+        }
+      }
+    } else {
+      uint8_t *y = q.dst + s * q.dst_stride + (kFft ? (1 + ch) * C * sb : 0);
+#pragma unroll
+      for (int jj = 0; jj < N; jj++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
+        if (act && p < n_dst) stp(row_rsrc(y + p * sb), so, v[jj]);
+      }
+    }
+  }
+}
+
 // ======================================================= low-rate encode (§8 f4)
 // The reference panics on low rate (root.zig:119-121); this is the encode of the
 // algorithm it ports (rs_gf.hpp scalar_encode_low, parity unpinned): the k originals are
@@ -1932,8 +2007,16 @@ KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv) {
     continue;                                                                     \
   }
 
+static hipError_t launch_encode_low_phases(const EncodeArgs &a, hipStream_t s);
+
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
   trace_launch(kc.name);
+  // phase launches where the per-lane column walk leaves the chip short of waves (fewer than
+  // 1,024 lane columns of 64: RS(1000,4000) 4 KiB x 64 2.78 -> 1.91 ms); with more, the walk's
+  // fewer launches win (RS(300,1000) 1 MiB x 16 32.7 vs 41.7 ms, 64 KiB x 8 1.29 vs 1.35 ms;
+  // profiles/r04/lowrate/encode_phases.log)
+  if (kc.variant == Variant::kGeneric && a.chunk >= 64 && a.n_stripes * (a.shard_bytes / 8) < 64ull * 1024)
+    return launch_encode_low_phases(a, s);
   if (kc.variant == Variant::kGeneric) {
     // a.scratch: `regions` C-position regions per stripe (low_encode): the coefficients, then
     // one per recovery chunk of a launch; the chunks run in groups of regions - 1
@@ -2203,6 +2286,95 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
                    : last        ? launch_dphase<false, kPhScatter, 30>(ph[i].n, g, a, q, s)
                                  : hipErrorInvalidValue;  // no fourth FFT phase below W = 2^19
     if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <int MODE, int NS>
+static hipError_t launch_ephase(uint32_t n, uint32_t ni, dim3 g, const EncodeArgs &a, const PhaseArgs &q, uint32_t subs,
+                                uint32_t fc, hipStream_t s) {
+  if (ni) {  // the first FFT phase with the IFFT's last phase: 64-point sub-problems
+    if constexpr (MODE == kEpFft) {  // (never also the last phase, never an IFFT phase)
+      if (n != 64) return hipErrorInvalidValue;
+      switch (ni) {
+#define RS_EPF_CASE(NI_) \
+  case NI_: hipLaunchKernelGGL((k_ephase<64, MODE, NI_>), g, dim3(kBlock), 0, s, a, q, subs, fc); break;
+        RS_EPF_CASE(2) RS_EPF_CASE(4) RS_EPF_CASE(8) RS_EPF_CASE(16) RS_EPF_CASE(32) RS_EPF_CASE(64)
+#undef RS_EPF_CASE
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    } else {
+      return hipErrorInvalidValue;
+    }
+  }
+  switch (n) {
+#define RS_EPH_CASE(N_)                                                                \
+  case N_:                                                                             \
+    if constexpr ((NS & N_) != 0) {                                                    \
+      hipLaunchKernelGGL((k_ephase<N_, MODE, 0>), g, dim3(kBlock), 0, s, a, q, subs, fc); \
+      break;                                                                           \
+    } else {                                                                           \
+      return hipErrorInvalidValue;                                                     \
+    }
+    RS_EPH_CASE(2) RS_EPH_CASE(4) RS_EPH_CASE(8) RS_EPH_CASE(16) RS_EPH_CASE(32) RS_EPH_CASE(64)
+#undef RS_EPH_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// rs_gf.hpp scalar_encode_low as phase launches (k_ephase); a.scratch: a.regions C-row
+// regions per stripe (coefficients + one per recovery chunk of a launch), chunk groups of
+// regions - 1 as launch_encode_low's generic path
+static hipError_t launch_encode_low_phases(const EncodeArgs &a, hipStream_t s) {
+  const uint64_t C = a.chunk, sb = a.shard_bytes, k = a.k;
+  if (C < 64 || (C & (C - 1)) || sb % 64) return hipErrorInvalidValue;
+  const uint32_t R = a.regions ? a.regions : 1 + a.n_chunks, G = R - 1;
+  if (G == 0) return hipErrorInvalidValue;
+  const uint64_t stride = static_cast<uint64_t>(R) * C * sb;
+  const bool contig = contig_ok(sb, 1);
+  const dim3 g0 = grid_for(sb, 1, 1);
+  const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
+  const uint64_t ri = std::min<uint64_t>(k, C);
+  std::vector<XPhase> iph, fph;
+  xform_phases(C, true, iph);
+  xform_phases(C, false, fph);
+  const bool fuse = iph.size() >= 2;
+  uint8_t *X = a.scratch;
+  uint64_t lim = 0;
+  for (size_t i = 0; i + (fuse ? 1 : 0) < iph.size(); i++) {
+    const uint64_t span = static_cast<uint64_t>(iph[i].n) << iph[i].dlo_log, wl = round_up(ri, span);
+    PhaseArgs q{X, X, stride, stride, i == 0 ? ri : lim, wl, sb, C, ri, iph[i].ti, a.tabs, iph[i].dlo_log, nullptr,
+                nullptr, contig, nullptr, 0, 0, 0};
+    const dim3 g(g0.x, static_cast<uint32_t>(wl / iph[i].n), gz);
+    hipError_t e = i == 0 ? launch_ephase<kEpGather, 64>(iph[i].n, 0, g, a, q, 0, 0, s)
+                          : launch_ephase<0, 64>(iph[i].n, 0, g, a, q, 0, 0, s);
+    if (e != hipSuccess) return e;
+    lim = wl;
+  }
+  const uint64_t TI = ifft_tab_count(C);
+  for (uint32_t j0 = 0; j0 < a.n_chunks; j0 += G) {
+    EncodeArgs b = a;
+    b.chunk0 = j0;
+    const uint32_t nc = std::min(G, a.n_chunks - j0);
+    for (size_t i = 0; i < fph.size(); i++) {
+      const bool first = i == 0, last = i + 1 == fph.size();
+      const uint32_t subs = static_cast<uint32_t>(C / fph[i].n);
+      if (static_cast<uint64_t>(subs) * nc > 65535) return hipErrorInvalidValue;
+      // first: reads region 0 (the coefficients, with the IFFT's last phase fused in when
+      // there is one); the others read their chunk's region
+      PhaseArgs q{X, X, stride, stride, first ? (fuse ? lim : C) : C, 0, sb, C, 0, fph[i].ti, a.tabs + TI,
+                  fph[i].dlo_log, nullptr, nullptr, contig, a.tabs, fuse ? iph.back().ti : 0, ri,
+                  fuse ? iph.back().dlo_log : 0};
+      const uint32_t ni = first && fuse ? iph.back().n : 0;
+      if (ni && (fph[i].n != 64 || (64u >> (iph.back().dlo_log - fph[i].dlo_log)) != ni)) return hipErrorInvalidValue;
+      const dim3 g(g0.x, subs * nc, gz);
+      const uint32_t fc = first ? 0u : 1u;
+      hipError_t e = last ? launch_ephase<kEpFft | kEpOut, 126>(fph[i].n, ni, g, b, q, subs, fc, s)
+                          : launch_ephase<kEpFft, 64>(fph[i].n, ni, g, b, q, subs, fc, s);
+      if (e != hipSuccess) return e;
+    }
   }
   return hipSuccess;
 }

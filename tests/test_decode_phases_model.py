@@ -260,3 +260,117 @@ def case(W, trunc, trunc_fft, seed):
 def test_phased_decode_matches_layer_walk(W, trunc, trunc_fft):
     src, dst = case(W, trunc, trunc_fft, W * 7 + trunc)
     assert decode_phased(src, W, trunc, trunc_fft, dst) == decode_ref(src, W, trunc, trunc_fft, dst)
+
+
+# ---- the low-rate encode's launch sequence (rs_kernels.hip launch_encode_low_phases)
+def encode_ref(data, C, k, m):
+    x = [data.get(p, 0) for p in range(C)]
+    ifft_ref(x, C, k)
+    out = {}
+    for j in range((m + C - 1) // C):
+        t = min(C, m - j * C)
+        y = list(x)
+        fft_ref_keyed(y, C, t, j)
+        for p in range(t):
+            out[j * C + p] = y[p]
+    return out
+
+
+def fft_ref_keyed(x, size, trunc, chunk):
+    """fft_ref with twiddles keyed by the chunk too (each chunk has its own skew)."""
+    lg = size.bit_length() - 1
+    d, d4 = 1 << (lg - 2) if lg >= 2 else 0, size
+    while d >= 1 and 4 * d == d4:
+        for r in range(0, min(trunc, size), 4 * d):
+            m01, m23, m02 = tw(("f", chunk, d, r, 0)), tw(("f", chunk, d, r, 2)), tw(("f", chunk, d, r, 1))
+            for i in range(r, r + d):
+                fft_bf(x, i, i + 2 * d, m02)
+                fft_bf(x, i + d, i + 3 * d, m02)
+                fft_bf(x, i, i + d, m01)
+                fft_bf(x, i + 2 * d, i + 3 * d, m23)
+        d4, d = d, d // 4
+    if d4 == 2:
+        for r in range(0, min(trunc, size), 2):
+            fft_bf(x, r, r + 1, tw(("f", chunk, 1, r, 9)))
+
+
+def fft_sub_keyed(v, N, rmax, blk, dlo_log, chunk):
+    jd4, jd = N, N >> 2
+    while jd != 0:
+        d = jd << dlo_log
+        for jr in range(0, N, jd4):
+            r = blk + (jr << dlo_log)
+            if r < rmax:
+                m01, m23, m02 = tw(("f", chunk, d, r, 0)), tw(("f", chunk, d, r, 2)), tw(("f", chunk, d, r, 1))
+                for i in range(jr, jr + jd):
+                    fft_bf(v, i, i + 2 * jd, m02)
+                    fft_bf(v, i + jd, i + 3 * jd, m02)
+                    fft_bf(v, i, i + jd, m01)
+                    fft_bf(v, i + 2 * jd, i + 3 * jd, m23)
+        jd4, jd = jd, jd >> 2
+    if jd4 == 2:
+        for jr in range(0, N, 2):
+            r = blk + jr
+            if r < rmax:
+                fft_bf(v, jr, jr + 1, tw(("f", chunk, 1, r, 9)))
+
+
+def encode_phased(data, C, k, m):
+    iph, fph = xform_phases(C, True), xform_phases(C, False)
+    fuse = len(iph) >= 2
+    NI, DI = iph[-1]
+    X = [None] * C
+    lim = 0
+    for i, (N, dl) in enumerate(iph[:-1] if fuse else iph):
+        span = N << dl
+        wl = round_up(k, span)
+        for sub in range(wl // N):
+            blk, lo = (sub >> dl) * span, sub & ((1 << dl) - 1)
+            ps = [blk + lo + (j << dl) for j in range(N)]
+            v = [data.get(p, 0) if p < k else 0 for p in ps] if i == 0 else [X[p] if p < lim else 0 for p in ps]
+            ifft_sub(v, N, C, k, blk, dl)
+            for j, p in enumerate(ps):
+                if p < wl:
+                    X[p] = v[j]
+        lim = wl
+    out = {}
+    for ch in range((m + C - 1) // C):
+        t = min(C, m - ch * C)
+        Y = [None] * C
+        for i, (N, dl) in enumerate(fph):
+            span = N << dl
+            first, last = i == 0, i + 1 == len(fph)
+            snap = list(Y)
+            for sub in range(C // N):
+                blk, lo = (sub >> dl) * span, sub & ((1 << dl) - 1)
+                if blk >= t:
+                    continue
+                ps = [blk + lo + (j << dl) for j in range(N)]
+                if first:
+                    v = [X[p] if (not fuse or p < lim) else 0 for p in ps] if fuse else [X[p] for p in ps]
+                    if fuse:
+                        G = N // NI
+                        for g in range(G):
+                            w = [v[g + u * G] for u in range(NI)]
+                            ifft_sub(w, NI, C, k, 0, DI)
+                            for u in range(NI):
+                                v[g + u * G] = w[u]
+                else:
+                    v = [snap[p] for p in ps]
+                fft_sub_keyed(v, N, t, blk, dl, ch)
+                n_dst = round_up(t, 1 << dl)
+                for j, p in enumerate(ps):
+                    if last:
+                        if p < t:
+                            out[ch * C + p] = v[j]
+                    elif p < n_dst:
+                        Y[p] = v[j]
+    return out
+
+
+@pytest.mark.parametrize("C,k,m", [(64, 40, 100), (128, 100, 300), (512, 300, 1000), (1024, 1000, 4000),
+                                   (256, 200, 56), (2048, 1500, 2100)])
+def test_phased_low_rate_encode_matches_layer_walk(C, k, m):
+    rng = random.Random(C + k + m)
+    data = {p: rng.getrandbits(64) for p in range(k)}
+    assert encode_phased(data, C, k, m) == encode_ref(data, C, k, m)
