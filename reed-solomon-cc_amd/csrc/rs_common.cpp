@@ -100,10 +100,18 @@ namespace host {
 std::mutex g_dev_mu;
 std::map<int, int> g_dev_ok;  // device -> RS_OK / RS_ERR_NO_DEVICE
 
+namespace {
+std::atomic<bool> g_process_exiting{false};
+void mark_process_exiting() { g_process_exiting.store(true); }
+}  // namespace
+bool process_exiting() { return g_process_exiting.load(); }
+
 int current_device(int *dev) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RS_ERR_NO_DEVICE, "no HIP device visible");
   HIP_TRY(hipGetDevice(dev));
+  static std::once_flag exit_once;  // after the runtime's initialisation: runs before its teardown
+  std::call_once(exit_once, [] { std::atexit(mark_process_exiting); });
   std::lock_guard<std::mutex> lk(g_dev_mu);
   auto it = g_dev_ok.find(*dev);
   if (it == g_dev_ok.end()) {

@@ -96,11 +96,15 @@ int check_codec(uint64_t k, uint64_t m, size_t shard_bytes);
 int align_nv(std::initializer_list<uint64_t> vals);
 
 // ------------------------------------------------------- plans (rs_common.cpp)
+// Set by an exit handler registered after the HIP runtime's (so it runs before the runtime's
+// teardown): the plan caches' static destruction then skips HIP calls (the process is ending;
+// freeing into a torn-down runtime can fault)
+bool process_exiting();
 struct DevBuf {
   void *p = nullptr;
   int dev = 0;
   ~DevBuf() {
-    if (p) {
+    if (p && !process_exiting()) {
       int cur = 0;
       (void)hipGetDevice(&cur);
       (void)hipSetDevice(dev);
