@@ -234,6 +234,7 @@ def c4_leg(dev, reps, n=512):
     res["reconstruct_cold"] = {"calls": calls, "pattern": "55 erased data shards, every third from 2",
                                "note": "first calls of a new pattern, no warm-up (plan build included in wall_ms)",
                                "verified": bool(torch.equal(out, data[:, lost_c]))}
+    R.net_wait()  # the cold pattern's queued upgrade finishes here, not during process exit
     del data, par, out
     torch.cuda.empty_cache()
     return res
