@@ -423,8 +423,8 @@ int rs_reconstruct_warm(uint64_t k, uint64_t m, size_t sb, const uint8_t *presen
     if (is_low_rate(k, m)) return low_warm(dev, k, m, psb, present);
     std::shared_ptr<DecodePlan> plan;
     if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan))) return st;
-    if (plan->lite) {  // the second use decides (and queues) the upgrade; wait for it
-      if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan))) return st;
+    if (plan->lite) {  // a later use decides (and queues) the upgrade; wait for it
+      if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan, 3))) return st;
       jit::wait_pending();
       if ((st = get_decode_plan(dev, k, m, psb, flags, present, plan))) return st;
     }

@@ -264,21 +264,40 @@ int twiddle_plan(int dev, uint64_t W, uint32_t flags, std::shared_ptr<DevBuf> &o
   return RS_OK;
 }
 
-// Plan uploads go through a private non-blocking stream per (thread, device): a
-// synchronous hipMemcpy runs on the null stream, which orders itself against every
-// blocking stream of the device — an upload from the background worker (a plan upgrade)
-// would then wait for the caller's in-flight batches and delay its next launches.
-// (The streams are never destroyed: a destructor at thread exit could run after the HIP
-// runtime's teardown)
+// Plan uploads go through private non-blocking streams: a synchronous hipMemcpy runs on the
+// null stream, which orders itself against every blocking stream of the device — an upload
+// from the background worker (a plan upgrade) would then wait for the caller's in-flight
+// batches and delay its next launches. A small fixed pool per device (created once, each
+// stream used under its own lock; ADVICE r4: one stream per thread leaked a stream per
+// short-lived thread). The streams are never destroyed: a destructor at exit could run after
+// the HIP runtime's teardown.
+namespace {
+constexpr int kUploadStreams = 4;
+struct UploadPool {
+  hipStream_t st[kUploadStreams] = {};
+  std::mutex mu[kUploadStreams];
+  std::atomic<uint32_t> next{0};
+};
+std::mutex g_upload_mu;
+std::map<int, UploadPool *> g_upload_pools;  // never freed (see above)
+}  // namespace
+
 int upload(const void *host, size_t bytes, int dev, std::shared_ptr<DevBuf> &out) {
-  thread_local std::map<int, hipStream_t> streams;
+  UploadPool *pool = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_upload_mu);
+    UploadPool *&p = g_upload_pools[dev];
+    if (!p) p = new UploadPool;
+    pool = p;
+  }
   auto b = std::make_shared<DevBuf>();
   b->dev = dev;
   HIP_TRY(dev_malloc(&b->p, std::max<size_t>(bytes, 16)));
-  hipStream_t &st = streams[dev];
-  if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  HIP_TRY(hipMemcpyAsync(b->p, host, bytes, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  const uint32_t i = pool->next.fetch_add(1) % kUploadStreams;
+  std::lock_guard<std::mutex> lk(pool->mu[i]);
+  if (!pool->st[i]) HIP_TRY(hipStreamCreateWithFlags(&pool->st[i], hipStreamNonBlocking));
+  HIP_TRY(hipMemcpyAsync(b->p, host, bytes, hipMemcpyHostToDevice, pool->st[i]));
+  HIP_TRY(hipStreamSynchronize(pool->st[i]));
   out = b;
   return RS_OK;
 }
@@ -333,7 +352,13 @@ int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules) {
   });
 }
 
-int64_t rs_debug_fail_alloc(int64_t n) { return arm_alloc_failure(n); }
+// The counter is process-wide: a plan upgrade or compile still queued from an earlier call
+// would otherwise take the armed index on the background worker, so the worker
+// is drained before arming.
+int64_t rs_debug_fail_alloc(int64_t n) {
+  jit::wait_pending();
+  return arm_alloc_failure(n);
+}
 
 int rs_debug_release_caches(uint64_t *pooled_contexts) {
   return guarded([&]() -> int {

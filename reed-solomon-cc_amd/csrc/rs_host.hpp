@@ -183,6 +183,7 @@ struct DecodePlan {
   // kernel, its next use has the full plan built on the background worker
   bool lite = false;
   std::atomic<bool> upgrading{false};
+  std::atomic<uint32_t> uses{1};  // calls that found this (lite) plan, the first included
 };
 
 // Plan caches: least-recently-used entries past RS_AMD_PLAN_CACHE (default 4096 per
@@ -270,9 +271,10 @@ void encode_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 void reconstruct_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
 int syndrome_map(uint64_t k, uint64_t m, const uint8_t *present, jit::NetSpec &ns);
 int get_encode_plan(int dev, uint64_t k, uint64_t m, uint32_t flags, std::shared_ptr<EncodePlan> &out);
-// how: 0 the cached plan (a lite plan schedules its upgrade when a network would win),
-// 1 never a lite plan (the fused kernel is unavailable), 2 build the full plan now (the
-// background upgrade)
+// how: 0 the cached plan (a lite plan schedules its upgrade when a network or the
+// pattern-compiled kernel would win; counts a use), 1 never a lite plan (the fused kernel is
+// unavailable), 2 build the full plan now (the background upgrade), 3 as 0 without counting
+// a use and without the reuse / worker-backlog bounds (rs_reconstruct_warm)
 int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags, const uint8_t *present,
                     std::shared_ptr<DecodePlan> &out, int how = 0);
 
@@ -318,6 +320,15 @@ bool fdec_supports(uint64_t k, uint64_t m, uint64_t sb, uint32_t flags);
 // RS_AMD_PDEC (default on): a reused wide-code pattern gets its pattern-compiled fused kernel
 constexpr uint64_t kPdecMaxK = 256;  // pattern-compiled fused reconstruct: codes up to k = 256
 bool pdec_enabled();
+// Bounds on the per-pattern compiles (each 1-16 s of hipRTC on the one background worker, and
+// a module that is never unloaded): a pattern is compiled in on its RS_AMD_PDEC_AFTER-th use
+// (default 3; rs_reconstruct_warm at once), at most RS_AMD_PDEC_MAX patterns per code and
+// device (default 32; later patterns keep the pattern-as-data kernel), and not while more
+// than RS_AMD_PDEC_QUEUE jobs (default 2) wait on the worker (a later use retries).
+uint32_t pdec_after();
+size_t pdec_queue();
+// admit the pattern `key` of code (dev, k, m) to the budget (true if already admitted)
+bool pdec_admit(int dev, uint64_t k, uint64_t m, const std::string &key);
 // exp, log, log_walsh in HBM (384 KiB per device)
 int device_tables(int dev, const uint16_t **exp, const uint16_t **log, const uint16_t **lw);
 

@@ -1058,6 +1058,11 @@ void compile_stats(uint64_t *compiles, uint64_t *disk_hits, uint64_t *modules) {
   }
 }
 
+size_t pending_jobs() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_pending.size();
+}
+
 void wait_pending() {
   std::unique_lock<std::mutex> lk(g_mu);
   g_cv.wait(lk, [] { return g_pending.empty(); });

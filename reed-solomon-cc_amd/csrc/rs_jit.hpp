@@ -106,6 +106,8 @@ void compile_stats(uint64_t *compiles, uint64_t *disk_hits, uint64_t *modules);
 
 // Block until no background compile or host job is running (rs_net_wait).
 void wait_pending();
+// compiles and host jobs queued or running on the background worker
+size_t pending_jobs();
 // Run `fn` on the background worker, in order with the compiles (the current device set),
 // once per key while pending; false if the worker is unavailable. At exit the queue is
 // dropped and a running job finishes before the HIP runtime's teardown (as a compile).

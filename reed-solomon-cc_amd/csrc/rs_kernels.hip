@@ -864,8 +864,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_generic(EncodeArgs a) {
 // ---- the generic reconstruct as a launch sequence (launch_decode_generic): one launch per
 // phase of xform_ph, the phase's sub-problems across the grid (y), so a small batch still
 // fills the chip. Grid: x = column units, y = sub-problem, z = stripes (strided).
-// Per stripe the scratch holds X (W positions: the IFFT, in place), A and B (the positions
-// the truncated FFT still needs after its first phase; decode_generic_rows). The steps ride
+// Per stripe the scratch holds X (W positions: the IFFT, in place; then A, written over X by
+// the first FFT phase) and B (the positions the truncated FFT still needs after its first
+// phase; decode_generic_rows). The steps ride
 // on the phases:
 //  * GATHER (first IFFT phase): positions come from the received shards * pre, zero where
 //    nothing was received (root.zig:291-303), instead of a staging pass;
@@ -954,6 +955,25 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
   const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
   for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
     Sym<1> v[N];
+    if constexpr ((MODE & kPhSplitB) != 0) {  // B = F1(X), the sub-problem without H: first,
+      // since A is then written over X (in place: the lane reads its positions before it
+      // writes them, and no other lane or workgroup touches them; decode_generic_rows)
+      const uint8_t *x = q.src + s * q.src_stride;
+      uint8_t *y = q.dst2 + s * q.dst_stride;
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
+        else dev::zero(v[j]);
+      }
+      ifft_last_in<N, NI>(v, q);
+      fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
+      }
+    }
     if constexpr ((MODE & kPhGather) != 0) {
       // the sub-problem's sources in one vector load (lane j: position j), then per position
       // a lane read and a load through a buffer resource with no records when nothing was
@@ -1057,23 +1077,6 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
       }
     } else {
       uint8_t *y = q.dst + s * q.dst_stride;
-#pragma unroll
-      for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
-      }
-    }
-    if constexpr ((MODE & kPhSplitB) != 0) {  // B = F1(X): the sub-problem again, without H
-      const uint8_t *x = q.src + s * q.src_stride;
-      uint8_t *y = q.dst2 + s * q.dst_stride;
-#pragma unroll
-      for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
-        else dev::zero(v[j]);
-      }
-      ifft_last_in<N, NI>(v, q);
-      fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
 #pragma unroll
       for (int j = 0; j < N; j++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
@@ -2201,8 +2204,11 @@ static uint64_t decode_y_rows(uint64_t W, uint64_t rmax_fft) {
   return ph.size() > 1 ? std::min(W, round_up(rmax_fft, 1ull << ph[0].dlo_log)) : 0;
 }
 
-uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft) {  // X | A | B
-  return W + 2 * decode_y_rows(W, trunc_fft ? trunc_fft : trunc);
+// X (A written over it in place) | B. The first FFT phase reads every position of its
+// sub-problem from X before it writes that sub-problem's A rows, and sub-problems are disjoint,
+// so A needs no buffer of its own (X | A | B took ~3W rows per stripe at W = 65536)
+uint64_t decode_generic_rows(uint64_t W, uint64_t trunc, uint64_t trunc_fft) {
+  return W + decode_y_rows(W, trunc_fft ? trunc_fft : trunc);
 }
 
 // NS: the sub-problem sizes a mode runs with for W = 64 .. 65536 (xform_phases): the first
@@ -2245,8 +2251,8 @@ static hipError_t launch_decode_generic(const DecodeArgs &a, hipStream_t s) {
   const uint64_t W = a.work, sb = a.shard_bytes;
   if (W < 2 || (W & (W - 1)) || W > 65536 || sb % 64) return hipErrorInvalidValue;
   const uint64_t ri = std::min<uint64_t>(a.trunc, W), rf = std::min<uint64_t>(a.trunc_fft ? a.trunc_fft : a.trunc, W);
-  const uint64_t ylen = decode_y_rows(W, rf), stride = (W + 2 * ylen) * sb;
-  uint8_t *X = a.scratch, *Y = a.scratch + W * sb, *B = Y + ylen * sb;
+  const uint64_t ylen = decode_y_rows(W, rf), stride = (W + ylen) * sb;
+  uint8_t *X = a.scratch, *Y = X, *B = X + W * sb;  // A in place over X (decode_generic_rows)
   const bool contig = contig_ok(sb, 1);
   const dim3 g0 = grid_for(sb, 1, 1);
   const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));

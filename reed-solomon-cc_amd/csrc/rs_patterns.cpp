@@ -71,6 +71,29 @@ bool pdec_enabled() {
   return fdec_mode() != 1 && !(e && std::strcmp(e, "0") == 0);
 }
 
+namespace {
+int env_num(const char *name, int def, int lo) {
+  const char *e = std::getenv(name);
+  return e && *e ? std::max(lo, std::atoi(e)) : def;
+}
+}  // namespace
+
+uint32_t pdec_after() { return static_cast<uint32_t>(env_num("RS_AMD_PDEC_AFTER", 3, 1)); }
+size_t pdec_queue() { return static_cast<size_t>(env_num("RS_AMD_PDEC_QUEUE", 2, 0)); }
+
+bool pdec_admit(int dev, uint64_t k, uint64_t m, const std::string &key) {
+  static std::mutex mu;
+  static std::map<std::string, std::set<std::string>> admitted;  // code -> pattern keys
+  const size_t cap = static_cast<size_t>(env_num("RS_AMD_PDEC_MAX", 32, 0));
+  const std::string code = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m);
+  std::lock_guard<std::mutex> lk(mu);
+  std::set<std::string> &s = admitted[code];
+  if (s.count(key)) return true;
+  if (s.size() >= cap) return false;
+  s.insert(key);
+  return true;
+}
+
 // corrected multiply only (under D1 the literal decode is no inverse of the encode), and
 // no code whose D2 encode drops a chunk (its parity is no codeword, so the result would
 // depend on which recovery rows are read; root.zig:268-335 reads all of them)

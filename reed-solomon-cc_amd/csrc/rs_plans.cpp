@@ -239,7 +239,8 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     if ((out = g_dec_plans.find(key))) {
       if (!out->lite) return RS_OK;
       if (!full && fdec_mode() == 1) return RS_OK;  // forced fused form: the block is all it needs
-      lite = out;  // the pattern's second use: build the full plan (network, tables) now
+      if (how == 0) out->uses++;
+      lite = out;  // a later use: build the full plan (network, tables) now if one is worth it
       out.reset();
     }
   }
@@ -288,15 +289,28 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
   // locator multiplies: no scalar-loaded masks); it replaces the syndrome
   // path's e x e network, and a direct network (few losses) stays ahead of it. k <= 256: the
   // compile grows with the code (RS(200,55) 8-16 s, RS(1000,64) 45 s of hipRTC per pattern)
-  const bool pdec_on = e > 0 && !every_lost && m <= 64 && k <= kPdecMaxK && pdec_enabled() &&
-                       fdec_supports(k, m, sb, flags) &&
-                       (mode == "auto" || mode == "net");
-  const bool syn_wins = !pdec_on && syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
+  // Only one steady-state kernel per pattern: a direct network (few losses) or this one
+  // (queuing both cost a compile whose kernel never ran). Per-pattern compiles are
+  // bounded (rs_host.hpp pdec_after / RS_AMD_PDEC_MAX / pdec_queue): a pattern seen fewer
+  // times, past its code's budget, or while the worker is backed up keeps the fused kernel
+  // with the pattern as data (a later use retries the last two).
+  const bool pdec_want = e > 0 && !every_lost && m <= 64 && k <= kPdecMaxK && pdec_enabled() &&
+                         fdec_supports(k, m, sb, flags) && (mode == "auto" || mode == "net") && !use_net &&
+                         !use_net_async;
+  const bool syn_wins = !pdec_want && syndrome_pick(k, m, e, flags, sb, mode) && 4 * e >= 3 * m;
+  if (lite && how != 2 && !full && pdec_want && !use_net && !use_net_async && !syn_wins &&
+      (lite->upgrading.load() ||
+       (how == 0 && (lite->uses.load() < pdec_after() || jit::pending_jobs() > pdec_queue())) ||
+       !pdec_admit(dev, k, m, key))) {
+    out = lite;  // not (yet) worth a compile, or already queued
+    return RS_OK;
+  }
+  const bool pdec_on = pdec_want && pdec_admit(dev, k, m, key);
   if (lite && !full && !use_net && !use_net_async && !syn_wins && !pdec_on) {
     out = lite;
     return RS_OK;
   }
-  if (lite && how == 0) {  // the full plan is built on the worker; the fused kernel meanwhile
+  if (lite && (how == 0 || how == 3)) {  // the full plan is built on the worker; the fused kernel meanwhile
     out = lite;
     if (!lite->upgrading.exchange(true)) {
       std::vector<uint8_t> pres(present, present + k + m);

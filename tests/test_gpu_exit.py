@@ -47,3 +47,40 @@ def test_exit_during_background_compile(tmp_path):
                        capture_output=True, text=True, timeout=240)
     assert "child done" in r.stdout, r.stderr[-2000:]
     assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+
+
+CHILD_PDEC = r"""
+import sys, torch
+sys.path.insert(0, %r)
+import reedsol_amd as R
+k, m, sb, n = 200, 55, 1 << 18, 8
+dev = torch.device("cuda:0")
+d = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8, device=dev)
+p = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
+R.encode_batch_dev(k, m, d, p)
+lost = list(range(2, k, 3))[:m]
+present = [0 if i in lost else 1 for i in range(k)] + [1] * m
+out = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
+for _ in range(3):  # the third use queues the upgrade: full plan build, then the pdecode compile
+    R.reconstruct_batch_dev(k, m, present, d, p, out)
+torch.cuda.synchronize()
+assert torch.equal(out, d[:, lost])
+print("child done", R.last_kernels(), flush=True)
+"""  # returns without rs_net_wait: the upgrade is queued or compiling, the plan caches hold device memory
+
+
+def test_exit_with_pattern_upgrade_in_flight(tmp_path):
+    """The round-4 bench fault: a process that ended while an RS(200,55) pattern's background
+    upgrade (plan build + the pattern-compiled kernel's hipRTC compile, 4-16 s) was queued, with
+    the plan caches holding device buffers, faulted in teardown. Since then an exit handler
+    registered after the HIP runtime's marks the process as exiting before that runtime is torn
+    down, the cached buffers' destructors skip hipFree, and the worker drops its queue and joins
+    the compile in flight. Exit code 0, with the compile in flight (empty disk cache)."""
+    env = dict(os.environ, RS_AMD_CACHE_DIR=str(tmp_path))
+    for v in ("RS_AMD_JIT_SYNC", "RS_AMD_PDEC_AFTER", "RS_AMD_FDEC", "RS_AMD_PDEC"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, "-c", CHILD_PDEC % os.path.join(ROOT, "reed-solomon-cc_amd")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert "child done" in r.stdout, r.stderr[-2000:]
+    assert "rs_fft_decode_k200_m55" in r.stdout, r.stdout  # the calls ran the pattern-as-data kernel
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])

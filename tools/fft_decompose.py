@@ -66,6 +66,7 @@ def main():
             kr = R.last_kernels()
             res[v]["ok_rec"] &= bool(torch.equal(out, data[:, lost]))
             res[v]["kern"] = ";".join(ke + kr)
+            print(f"round {r} {dict(v)} enc {te:.3f} rec {tr:.3f}", file=sys.stderr, flush=True)
             if r > 0:
                 res[v]["enc"].append(te)
                 res[v]["rec"].append(tr)

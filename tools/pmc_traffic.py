@@ -20,7 +20,7 @@ def short_name(full):
     m = re.search(r"rs_net_(encode|reconstruct|syndrome)_i(\d+)_o(\d+)_[0-9a-f]+", full)
     if m:
         return f"net_{m.group(1)}_i{m.group(2)}_o{m.group(3)}"
-    m = re.search(r"rs_fft_(encode|decode|inverse)_k(\d+)_m(\d+)_[0-9a-f]+", full)
+    m = re.search(r"rs_fft_(encode|decode|pdecode|inverse)_k(\d+)_m(\d+)_[0-9a-f]+", full)
     if m:
         return f"net_fft_{m.group(1)}_i{m.group(2)}_o{m.group(3)}"
     m = re.search(r"k_(encode_reg|decode_reg|decode_matrix)<(\d+), (\d+)>", full)
