@@ -132,6 +132,7 @@ inline void ifft_bf_s(uint16_t &x, uint16_t &y, uint16_t lm, bool q) {
   y ^= x;
   if (lm != kModulus) x ^= mul_engine(y, lm, q);
 }
+}  // namespace
 void scalar_ifft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool q) {
   const uint16_t *sk = tables().skew;
   uint64_t d = 1;
@@ -168,7 +169,6 @@ void scalar_fft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool q)
   if (d4 == 2)
     for (uint64_t r = 0; r < trunc; r += 2) fft_bf_s(s[r], s[r + 1], sk[r + sd], q);
 }
-}  // namespace
 
 void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *er) {
   const uint64_t C = ceil_pow2(m), end = C + k;

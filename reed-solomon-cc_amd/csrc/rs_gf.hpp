@@ -96,6 +96,10 @@ void scalar_encode_low(const uint16_t *in, uint64_t k, uint64_t m, bool quirk_d1
 // missing original i x g^(65535 - e_i). `received` has W entries in this position layout.
 void erasure_logs_low(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *out);
 void scalar_reconstruct_low(uint16_t *sym, const uint8_t *received, const uint16_t *erasures, uint64_t k, uint64_t m);
+// Generic.zig:80-147 / 15-78 on one symbol per position (pos 0, skew_delta sd, size points,
+// groups r >= trunc skipped)
+void scalar_ifft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool quirk_d1);
+void scalar_fft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool quirk_d1);
 // IFFT chunk truncations of the encode schedule (root.zig:143-166; D2 drops the last full chunk)
 std::vector<uint64_t> encode_chunk_truncs(uint64_t k, uint64_t m, bool quirk_d2);
 // root.zig:277-289: erasure flags for a received pattern -> evalPoly -> logs (65536 entries)

@@ -299,6 +299,13 @@ int low_warm(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *presen
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb);
 const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e);
 int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
+// the low-rate reconstruct in block form (rs_lowrate.cpp): the scalars alpha_K, beta_K of the
+// W / C blocks, and the form on one symbol per position (host check); codes with at most
+// kLowBlockMaxBlocks blocks
+constexpr uint64_t kLowBlockMaxBlocks = 64;
+void low_block_coefs(uint64_t k, uint64_t m, std::vector<uint16_t> &alpha, std::vector<uint16_t> &beta);
+bool scalar_reconstruct_low_blocks(uint16_t *data, const uint16_t *par, const uint8_t *present, uint64_t k,
+                                   uint64_t m);
 void encode_low_map(uint64_t k, uint64_t m, uint32_t flags, jit::NetSpec &ns);
 
 // -------------------------------------------------------- patterns (rs_patterns.cpp)

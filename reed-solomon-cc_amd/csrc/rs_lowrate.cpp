@@ -173,8 +173,10 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
   uint64_t e = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   const bool net = map_net_ok(k, e, sb);
+  const char *te = std::getenv("RS_AMD_LOW_TRIM");
+  const bool trim = !(te && std::strcmp(te, "0") == 0);
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                    std::to_string(net) + "/" + std::to_string(jit::max_blocks()) + "/";
+                    std::to_string(net) + "/" + std::to_string(jit::max_blocks()) + "/" + (trim ? "t/" : "a/");
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   {
@@ -185,12 +187,20 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
   auto p = std::make_shared<LowDecodePlan>();
   const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end);
   p->W = static_cast<uint32_t>(W);
-  p->trunc = static_cast<uint32_t>(end);
   if (int st = twiddle_plan(dev, W, 0, p->tw, p->off_fft)) return st;
-  // position layout of scalar_reconstruct_low: originals [0, k), recovery [C, C + m)
+  // position layout of scalar_reconstruct_low: originals [0, k), recovery [C, C + m). Only
+  // the first e present recovery rows are read (round 5): with the k - e present originals and
+  // the known zeros [k, C) that is exactly C known positions, the dimension of the code, and
+  // the restored originals are the same; the other present rows join the erasures. Nothing is
+  // received past the last row read, so the IFFT is truncated there (its groups past it are
+  // all zero, Generic.zig:80-147), and its gather reads k rows instead of every present one.
+  // (RS_AMD_LOW_TRIM=0: every present row, the IFFT truncated at C + m, as before round 5)
   std::vector<uint8_t> received(W, 0);
   for (uint64_t i = 0; i < k; i++) received[i] = present[i] ? 1 : 0;
-  for (uint64_t r = 0; r < m; r++) received[C + r] = present[k + r] ? 1 : 0;
+  uint64_t last = k, nr = 0;
+  for (uint64_t r = 0; r < m && (nr < e || !trim); r++)
+    if (present[k + r]) received[C + r] = 1, nr++, last = C + r + 1;
+  p->trunc = static_cast<uint32_t>(trim ? last : end);
   std::vector<uint16_t> er(kOrder);
   erasure_logs_low(received.data(), k, m, er.data());
   std::vector<RsTab> tabs(2 * W);  // pre, post
@@ -346,6 +356,108 @@ int low_warm(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *presen
   return RS_OK;
 }
 
+// ---- the low-rate reconstruct in block form (round 5). Decoding the residual codeword
+// (received ^ the codeword of d' = the received originals with the erased ones zero) gives the
+// erased originals; its only non-zero inputs are the syndromes s = rec ^ Enc(d') on the
+// recovery rows R used (the first e present: exactly C positions are then known, the code's
+// dimension; the other present rows join the erasures). Those rows sit in blocks K >= 1 of
+// C positions; the outputs in block 0. Tracking the W-point decode block by block: the IFFT's
+// layers below C are per-block IFFT_{C, skew KC}; its layers >= C, the derivative's bits >= C
+// and the FFT's layers >= C only combine whole blocks with scalar factors, and the derivative's
+// bits below C act inside a block (D_C). So block 0 after the FFT's top layers is
+//   D_C(sum_K alpha_K b_K) + sum_K beta_K b_K,   b_K = IFFT_{C, skew KC}(L_R s_R in block K)
+// and the erased original g is g^(65535 - e_g) FFT_{C, skew 0, trunc k}(that)_g. The scalars
+// come from running the top layers' schedule on block coefficients (Generic.zig:15-147,
+// root.zig:306-312); the host selftest checks the form against scalar_reconstruct_low.
+namespace {
+uint16_t gm(uint16_t x, uint16_t y) { return x && y ? mul16(x, tables().log[y]) : 0; }
+uint16_t tw(uint64_t idx) {  // the element a butterfly at skew index idx multiplies by (0: XOR-only)
+  const uint16_t l = idx < kModulus ? tables().skew[idx] : static_cast<uint16_t>(kModulus);
+  return l == kModulus ? 0 : tables().exp[l];
+}
+}  // namespace
+
+void low_block_coefs(uint64_t k, uint64_t m, std::vector<uint16_t> &alpha, std::vector<uint16_t> &beta) {
+  const uint64_t C = ceil_pow2(k), W = ceil_pow2(C + m), nb = W / C;
+  std::vector<std::vector<uint16_t>> lam(nb, std::vector<uint16_t>(nb, 0));
+  for (uint64_t J = 0; J < nb; J++) lam[J][J] = 1;
+  auto axpy = [&](std::vector<uint16_t> &y, uint16_t t, const std::vector<uint16_t> &x) {  // y ^= t x
+    for (uint64_t K = 0; K < nb; K++) y[K] ^= gm(t, x[K]);
+  };
+  for (uint64_t d = C; d < W; d *= 2)  // IFFT layers >= C: y ^= x; x ^= t y (Generic.zig:171-192)
+    for (uint64_t g = 0; g < W; g += 2 * d) {
+      const uint16_t t = tw(g + d - 1);
+      for (uint64_t i = g; i < g + d; i += C) {
+        auto &x = lam[i / C], &y = lam[(i + d) / C];
+        for (uint64_t K = 0; K < nb; K++) y[K] ^= x[K];
+        axpy(x, t, y);
+      }
+    }
+  // block J = D_C(P_J) + Q_J: the derivative's bits >= C add whole blocks (root.zig:306-312)
+  std::vector<std::vector<uint16_t>> P = lam, Q(nb, std::vector<uint16_t>(nb, 0));
+  for (uint64_t J = 0; J < nb; J++)
+    for (uint64_t b = 1; b < nb; b <<= 1)
+      if (!(J & b) && J + b < nb)
+        for (uint64_t K = 0; K < nb; K++) Q[J][K] ^= lam[J + b][K];
+  for (uint64_t d = W / 2; d >= C && d > 0; d /= 2)  // FFT layers >= C: x ^= t y; y ^= x (Generic.zig:149-169)
+    for (uint64_t g = 0; g < W; g += 2 * d) {
+      const uint16_t t = tw(g + d - 1);
+      for (uint64_t i = g; i < g + d; i += C) {
+        const uint64_t x = i / C, y = (i + d) / C;
+        axpy(P[x], t, P[y]);
+        axpy(Q[x], t, Q[y]);
+        for (uint64_t K = 0; K < nb; K++) P[y][K] ^= P[x][K], Q[y][K] ^= Q[x][K];
+      }
+    }
+  alpha = P[0];
+  beta = Q[0];
+}
+
+// The block form on one symbol per position: data k (erased entries ignored), par m,
+// present k + m; restores data[g] for every erased g. Returns false if fewer than k present.
+bool scalar_reconstruct_low_blocks(uint16_t *data, const uint16_t *par, const uint8_t *present, uint64_t k,
+                                   uint64_t m) {
+  const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end), nb = W / C;
+  uint64_t e = 0;
+  for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
+  std::vector<uint8_t> received(W, 0), inR(m, 0);
+  for (uint64_t i = 0; i < k; i++) received[i] = present[i] ? 1 : 0;
+  uint64_t nr = 0;
+  for (uint64_t r = 0; r < m && nr < e; r++)
+    if (present[k + r]) received[C + r] = inR[r] = 1, nr++;
+  if (nr < e) return false;
+  std::vector<uint16_t> er(kOrder);
+  erasure_logs_low(received.data(), k, m, er.data());
+  std::vector<uint16_t> alpha, beta;
+  low_block_coefs(k, m, alpha, beta);
+  std::vector<uint16_t> coef(C, 0), U(C, 0), V(C, 0), b(C);
+  for (uint64_t i = 0; i < k; i++) coef[i] = present[i] ? data[i] : 0;
+  scalar_ifft(coef.data(), C, k, 0, false);  // the low-rate encode of d' (scalar_encode_low)
+  for (uint64_t K = 1; K < nb; K++) {
+    bool any = false;
+    for (uint64_t q = 0; q < C && (K - 1) * C + q < m; q++) any |= inR[(K - 1) * C + q] != 0;
+    if (!any) continue;
+    b = coef;
+    scalar_fft(b.data(), C, std::min(C, m - (K - 1) * C), K * C, false);  // Enc(d') rows of block K
+    for (uint64_t q = 0; q < C; q++) {
+      const uint64_t r = (K - 1) * C + q;
+      b[q] = r < m && inR[r] ? mul16(static_cast<uint16_t>(par[r] ^ b[q]), er[C + r]) : 0;
+    }
+    scalar_ifft(b.data(), C, C, K * C, false);
+    for (uint64_t q = 0; q < C; q++) U[q] ^= gm(alpha[K], b[q]), V[q] ^= gm(beta[K], b[q]);
+  }
+  for (uint64_t q = 0; q < C; q++) {  // D_C, ascending (reads original values above)
+    uint16_t z = U[q];
+    for (uint64_t w = 1; w < C; w <<= 1)
+      if (!(q & w)) z ^= U[q + w];
+    V[q] ^= z;
+  }
+  scalar_fft(V.data(), C, k, 0, false);
+  for (uint64_t g = 0; g < k; g++)
+    if (!present[g]) data[g] = mul16(V[g], static_cast<uint16_t>(kModulus - er[g]));
+  return true;
+}
+
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb) {
   if (map_net_ok(k, m, sb)) return net_name("encode_low", k, m);
   return choose_encode_low(ceil_pow2(k), sb, 4).name;
@@ -403,6 +515,14 @@ extern "C" int rs_lowrate_selftest(uint64_t k, uint64_t m, int trials, uint64_t 
       scalar_reconstruct_low(sym.data(), received.data(), er.data(), k, m);
       for (uint64_t i = 0; i < k; i++)
         if (!present[i] && sym[i] != data[i]) bad++;
+      // the block form (syndromes of the first e present recovery rows, C-point transforms)
+      if (W / C > kLowBlockMaxBlocks) continue;
+      std::vector<uint16_t> blk = data;
+      for (uint64_t i = 0; i < k; i++)
+        if (!present[i]) blk[i] = static_cast<uint16_t>(rnd());
+      if (!scalar_reconstruct_low_blocks(blk.data(), par.data(), present.data(), k, m)) bad++;
+      for (uint64_t i = 0; i < k; i++)
+        if (blk[i] != data[i]) bad++;
     }
     if (mismatches) *mismatches = bad;
     return RS_OK;

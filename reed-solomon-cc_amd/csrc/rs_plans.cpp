@@ -320,9 +320,13 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
             std::shared_ptr<DecodePlan> p;
             if (get_decode_plan(dev, k, m, sb, flags, pres.data(), p, 2) != RS_OK || !p) return;
             if (p->net) queue_net(*p->net, sb);
-            if (p->pdec) {
-              const fftnet::Spec *fs = nullptr;
-              (void)fft_kernel(*p->pdec, sb, &fs);
+            if (p->pdec) {  // compiled here, on the worker (a build that spills is rebuilt with
+              // less prefetch at once, not at the pattern's next call); the slot's async lookup
+              // then finds it in the module cache
+              fftnet::Spec ps = p->pdec->spec;
+              std::string err;
+              bool pending = false;
+              (void)fftnet::get(ps, false, err, pending);
             }
           }))
         lite->upgrading = false;

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 5: low-rate reconstruct reading k rows (first e present recovery rows) with the IFFT
+# truncated at the last row read; parity (low-rate tests, fuzz), then rates against
+# RS_AMD_LOW_TRIM=0 (every present row, the round-4 form), interleaved in one process.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/r5; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -m gpu \
+  tests/test_lowrate.py tests/test_gpu_fuzz.py > gpurun_out/r5/low_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/r5/low_tests.log; exit 1; }
+tail -2 gpurun_out/r5/low_tests.log
+: > gpurun_out/r5/low_rates.log
+for a in "200 1000 65536 8 100:0:2" "300 1000 65536 8 100:0:3" "1000 4000 4096 64 300:0:3" "300 1000 1048576 16 100:0:3" "100 600 65536 16 50:0:2"; do
+  set -- $a
+  timeout -k 10 300 python -u tools/kernel_sweep.py --k $1 --m $2 --shard-bytes $3 --stripes $4 --erase $5 --nv 4 \
+    --rounds 3 --reps 3 --wait --var RS_AMD_LOW_TRIM=1,0 >> gpurun_out/r5/low_rates.log 2>&1 || { echo "SWEEP FAILED: $a"; tail -5 gpurun_out/r5/low_rates.log; exit 1; }
+done
+grep -E '^\{' gpurun_out/r5/low_rates.log | cut -c1-330
