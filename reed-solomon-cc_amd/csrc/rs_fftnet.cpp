@@ -377,11 +377,6 @@ int vmask_of() { return env_int("RS_AMD_FFT_VMASK", 1) ? 1 : 0; }
 // RS(200,55) max_e 55 7.35 -> 6.66 ms, RS(16,16) 2.79 -> 2.71 ms (profiles/r04/patterns/rmul_ab.log).
 // Measured and removed: the masks through vector loads (7.35 -> 8.9 ms), s_setprio turns
 // between the SIMD-pair halves (c4 neutral to 8 % slower, profiles/r04/prio1.log)
-// static s_setprio for the second-dispatched half of the workgroup (waves 4-7 share SIMDs
-// with waves 0-3 and lose VALU arbitration to them; MI355X_MICROARCH.md, two waves per SIMD,
-// item 4): RS_AMD_FFT_SPRIO=1 raises waves 4-7 once at the start (0: off)
-int sprio_of() { return env_int("RS_AMD_FFT_SPRIO", 0); }
-
 int rmul_group() {
   const int g = env_int("RS_AMD_FFT_RMULG", 4);
   return g == 2 || g == 4 || g == 8 ? g : 1;
@@ -698,8 +693,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
     << (vmask_of() ? "  asm volatile(\"\" : \"+v\"(KM.f), \"+v\"(KM.t), \"+v\"(KM.s));\n" : "")
     << "  const u32 lane = threadIdx.x & 63u, ll = lane & 31u;\n"
        "  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-    << (sprio_of() == 1 ? "  if (w >= 4u) __builtin_amdgcn_s_setprio(1);\n" : sprio_of() == 2 ? "  if (w < 4u) __builtin_amdgcn_s_setprio(1);\n" : "")
-    << "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
+       "  const u32 loff = (ll >> 1) * 64u + (lane >= 32u ? 32u : 0u) + (ll & 1u) * 16u;\n"
        // unit u = stripe * ups + uu, walked with SALU counters (no 64-bit division in the loop)
     << (s.blocked ?
        // blocked walk: workgroup b takes units [b per, (b + 1) per), a stripe's units in a row
@@ -1454,7 +1448,7 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
   std::string k = "fft4:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":d" +
-                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":k" + std::to_string(vmask_of()) + ":q" + std::to_string(sprio_of()) + ":" +
+                  std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":k" + std::to_string(vmask_of()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
                   (s.pieces > 1 ? "p" + std::to_string(s.pieces) + ":" : "") + (s.inverse ? "inv:" : "") +
