@@ -202,14 +202,19 @@ const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_c
 
 /* Per-pattern kernels of wide codes compile in a background thread. A wide-code pattern's
  * first calls run the fused FFT reconstruct with the pattern as data (rs_fft_decode_*,
- * nothing compiled per pattern); its second call queues the full plan's build and, behind
- * it, the compile of its steady-state kernel on the background worker: the fused kernel
- * with the pattern compiled in (rs_fft_pdecode_*, k <= 256; RS(200,55): 8-16 s of hipRTC),
- * or a network where one beats it (few losses: the direct map; RS_AMD_FDEC=0: the e x e
- * syndrome map), and the calls run the first form until it is loaded. rs_net_wait blocks until the worker is idle
- * (no plan build or compile queued or running): after two calls + rs_net_wait the next
- * call runs the pattern's steady-state kernel. RS_AMD_JIT_SYNC=1 compiles in the calling
- * thread instead. Returns RS_OK. */
+ * nothing compiled per pattern). One steady-state kernel per pattern is then built on the
+ * background worker, behind the full plan's build: a network where one beats the fused
+ * kernel (few losses: the direct map, queued at the pattern's second call; RS_AMD_FDEC=0:
+ * the e x e syndrome map), else the fused kernel with the pattern compiled in
+ * (rs_fft_pdecode_*, k <= 256; RS(200,55): 8-16 s of hipRTC), queued at the pattern's
+ * RS_AMD_PDEC_AFTER-th call (default 3). The pattern-compiled kernels are bounded: at most
+ * RS_AMD_PDEC_MAX (default 32) patterns per code and device (later patterns keep the
+ * pattern-as-data kernel), and none is queued while more than RS_AMD_PDEC_QUEUE (default 2)
+ * jobs wait on the worker (a later call retries). The calls run the first form until the
+ * steady-state kernel is loaded. rs_net_wait blocks until the worker is idle (no plan build
+ * or compile queued or running): after three calls + rs_net_wait the next call runs the
+ * pattern's steady-state kernel (rs_reconstruct_warm gets there at once). RS_AMD_JIT_SYNC=1
+ * compiles in the calling thread instead. Returns RS_OK. */
 int rs_net_wait(void);
 
 /* Drive one erasure pattern of rs_reconstruct_batch_dev (same arguments) to its steady
@@ -321,6 +326,11 @@ const uint16_t *rs_table_exp(void);       /* [65536] */
 const uint16_t *rs_table_log(void);       /* [65536] */
 const uint16_t *rs_table_skew(void);      /* [65535] */
 const uint16_t *rs_table_log_walsh(void); /* [65536] */
+/* tables.zig:94-118 `mul_128: [65536]Lut`, `Lut = [2][4]u128`: for multiplier log_m, byte
+ * [log_m][h][i][j] = byte h (0 low, 1 high) of mul16(j << 4i, log_m) — the x86 engine's
+ * pshufb nibble tables (8 MiB, built on the first call; the GPU kernels use their own
+ * v_perm / bit-sliced forms). NULL if it cannot be allocated. */
+const uint8_t *rs_table_mul_128(void);
 
 #ifdef __cplusplus
 }

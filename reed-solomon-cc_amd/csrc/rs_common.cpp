@@ -344,6 +344,21 @@ const uint16_t *rs_table_exp(void) { return tables().exp; }
 const uint16_t *rs_table_log(void) { return tables().log; }
 const uint16_t *rs_table_skew(void) { return tables().skew; }
 const uint16_t *rs_table_log_walsh(void) { return tables().log_walsh; }
+const uint8_t *rs_table_mul_128(void) {  // tables.zig:94-118
+  static const uint8_t *t = []() -> const uint8_t * {
+    uint8_t *p = static_cast<uint8_t *>(std::malloc(size_t(kOrder) * 128));
+    if (!p) return nullptr;
+    for (uint32_t lm = 0; lm < kOrder; lm++)
+      for (uint32_t i = 0; i < 4; i++)
+        for (uint32_t j = 0; j < 16; j++) {
+          const uint16_t prod = mul16(static_cast<uint16_t>(j << (4 * i)), static_cast<uint16_t>(lm));
+          p[size_t(lm) * 128 + i * 16 + j] = static_cast<uint8_t>(prod);
+          p[size_t(lm) * 128 + 64 + i * 16 + j] = static_cast<uint8_t>(prod >> 8);
+        }
+    return p;
+  }();
+  return t;
+}
 
 int rs_jit_stats(uint64_t *compiles, uint64_t *cache_hits, uint64_t *modules) {
   return guarded([&]() -> int {

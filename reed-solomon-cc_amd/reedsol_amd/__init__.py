@@ -110,6 +110,7 @@ def lib():
         "rs_table_log": (u16p, []),
         "rs_table_skew": (u16p, []),
         "rs_table_log_walsh": (u16p, []),
+        "rs_table_mul_128": (C.POINTER(C.c_uint8), []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -479,7 +480,13 @@ def engine_eval_poly(erasures, truncated_size: int):
 
 
 def table(name: str):
+    """tables.zig: exp / log / skew / log_walsh (u16), or mul_128 ([65536][2][4][16] u8)."""
     import numpy as np
+    if name == "mul_128":
+        p = lib().rs_table_mul_128()
+        if not p:
+            raise MemoryError("rs_table_mul_128")
+        return np.ctypeslib.as_array(p, shape=(65536, 2, 4, 16)).copy()
     n = {"exp": 65536, "log": 65536, "skew": 65535, "log_walsh": 65536}[name]
     p = getattr(lib(), "rs_table_" + name)()
     return np.ctypeslib.as_array(p, shape=(n,)).copy()

@@ -36,6 +36,13 @@ def test_tables_match_oracle(oracle):
         assert (R.table(name) == oracle.table(name)).all(), name
 
 
+def test_mul_128_matches_oracle(oracle):
+    """tables.zig:94-118 mul_128 (the Lut seam) through the C ABI == the oracle's table."""
+    got = R.table("mul_128")
+    assert got.shape == (65536, 2, 4, 16)
+    assert (got.reshape(-1) == oracle.mul128().reshape(-1)).all()
+
+
 @pytest.mark.parametrize("k,m", [(10, 4), (5, 5), (3, 4), (4, 3), (2, 4), (0, 4), (4, 0), (65537, 1),
                                  (32768, 32768), (32769, 32768), (200, 55), (1, 1), (65536, 1)])
 def test_use_high_rate_matches_oracle(oracle, k, m):
