@@ -302,7 +302,7 @@ int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *presen
 // the low-rate reconstruct in block form (rs_lowrate.cpp): the scalars alpha_K, beta_K of the
 // W / C blocks, and the form on one symbol per position (host check); codes with at most
 // kLowBlockMaxBlocks blocks
-constexpr uint64_t kLowBlockMaxBlocks = 64;
+constexpr uint64_t kLowBlockMaxBlocks = 512;
 void low_block_coefs(uint64_t k, uint64_t m, std::vector<uint16_t> &alpha, std::vector<uint16_t> &beta);
 bool scalar_reconstruct_low_blocks(uint16_t *data, const uint16_t *par, const uint8_t *present, uint64_t k,
                                    uint64_t m);

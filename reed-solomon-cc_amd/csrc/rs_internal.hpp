@@ -123,6 +123,28 @@ KernelChoice choose_decode_w(uint64_t W, uint64_t shard_bytes, int max_nv);  // 
 // (scratch [stripe][2C][sb]).
 KernelChoice choose_encode_low(uint64_t C, uint64_t shard_bytes, int max_nv);
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
+
+// Low-rate reconstruct in block form (rs_lowrate.cpp, C = ceilPow2(k) >= 128): C-point
+// transforms only. enc: originals (erased ones flagged in enc.skip), tabs = the low-rate
+// encode's tables for chunks j < n_chunks (enc.m = m' = the last recovery row used + 1),
+// scratch [stripe][low_block_rows(C, k)][sb]. dec: out / out_stripe_stride, tab_fft =
+// FFT(C, skew 0), tab_post / pos_dst per position < C (the erased originals). Per block
+// K = j + 1: syn_idx[jC + p] >= 0 for the recovery rows used, syn_tab[jC + p] their multiplier
+// L_r sigma_K, tabs_i + j * ifft_tab_count(C) = IFFT(C, skew KC), gamma[j] and u[j] (host)
+// the block's scalars.
+struct LowBlockArgs {
+  EncodeArgs enc;
+  DecodeArgs dec;
+  const uint8_t *rec;
+  uint64_t rec_stripe_stride;
+  const int32_t *syn_idx;
+  const RsTab *syn_tab;
+  const RsTab *tabs_i;
+  const RsTab *gamma;
+  const uint8_t *u;
+};
+uint64_t low_block_rows(uint64_t C, uint64_t k);
+hipError_t launch_low_blocks(const LowBlockArgs &a, hipStream_t s);
 // reconstruct as an n_out x n_in matrix of GF(2)-linear maps (decode matrix + GF MAC)
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv);
 constexpr uint32_t kMatrixMaxOut = 8;

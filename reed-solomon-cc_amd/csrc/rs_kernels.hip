@@ -902,6 +902,11 @@ struct PhaseArgs {
   const RsTab *tabs_i;
   uint64_t ti_i, rmax_i;
   uint32_t dlo_i;
+  // k_ephase SYN (low-rate block form): the recovery rows and the syndrome multipliers
+  const uint8_t *rec = nullptr;
+  uint64_t rec_stride = 0;
+  const int32_t *syn_idx = nullptr;
+  const RsTab *syn_tab = nullptr;
 };
 
 // The IFFT's last phase inside the first FFT phase's sub-problem: that sub-problem (fixed
@@ -1093,7 +1098,10 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 // the recovery rows jC + p directly. The IFFT's last phase runs inside the first FFT
 // phase's loads (as launch_decode_generic does), so region 0 is read, never rewritten, by
 // every chunk. Grid y = (chunk of the launch, sub-problem) for the FFT phases.
-enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4 };
+// SYN (the low-rate reconstruct in block form, launch_low_blocks): the last FFT phase of block
+// K = j + 1 forms the residual's syndromes instead of storing recovery rows, and the gather
+// reads the originals flagged in a.skip (the erased ones) as zero.
+enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4, kEpSyn = 8 };
 
 template <int N, int MODE, int NI>
 __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, uint32_t subs, uint32_t from_chunk) {
@@ -1120,7 +1128,8 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
 #pragma unroll
       for (int jj = 0; jj < N; jj++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
-        const __amdgpu_buffer_rsrc_t r = p < q.n_src ? row_rsrc(d + p * sb) : zero_rsrc();
+        const bool rd = p < q.n_src && !skipped(a, static_cast<uint32_t>(p));
+        const __amdgpu_buffer_rsrc_t r = rd ? row_rsrc(d + p * sb) : zero_rsrc();
         v[jj].l[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io, 0, 0);
         v[jj].h[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io_h, 0, 0);
       }
@@ -1138,7 +1147,44 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
     }
     if constexpr (kFft) fft_sub<N, 1>(v, tabs, q.ti, C, rmax, blk, q.dlo_log);
     else ifft_sub<N, 1>(v, tabs, q.ti, C, rmax, blk, q.dlo_log);
-    if constexpr ((MODE & kEpOut) != 0) {
+    if constexpr ((MODE & kEpSyn) != 0) {
+      // recovery row r = jC + p: (rec_r ^ Enc(d')_r) L_r sigma_K where r is a row used, else
+      // zero; the rows in groups of 8 loads (lane jj holds position jj's row flag)
+      const uint8_t *rc = q.rec + s * q.rec_stride + j * C * sb;
+      const int32_t *si = q.syn_idx + j * C;
+      const RsTab *st = q.syn_tab + j * C;
+      uint8_t *y = q.dst + s * q.dst_stride + (1 + ch) * C * sb;
+      const uint32_t ln = __lane_id();
+      const uint64_t lp = blk + lo + (static_cast<uint64_t>(ln) << q.dlo_log);
+      const int32_t my = ln < static_cast<uint32_t>(N) && lp < rmax ? si[lp] : -1;
+      constexpr int G8 = N < 8 ? N : 8;
+#pragma unroll
+      for (int g0 = 0; g0 < N; g0 += G8) {
+        Sym<1> t[G8];
+#pragma unroll
+        for (int jj = 0; jj < G8; jj++) {
+          const uint64_t p = blk + lo + (static_cast<uint64_t>(g0 + jj) << q.dlo_log);
+          const bool used = __builtin_amdgcn_readlane(my, g0 + jj) >= 0;
+          const __amdgpu_buffer_rsrc_t r = used ? row_rsrc(rc + p * sb) : zero_rsrc();  // wave-uniform
+          t[jj].l[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io, 0, 0);
+          t[jj].h[0] = __builtin_amdgcn_raw_buffer_load_b32(r, io_h, 0, 0);
+        }
+        if (q.contig)
+#pragma unroll
+          for (int jj = 0; jj < G8; jj++) dev::pair_halves(t[jj], true);
+#pragma unroll
+        for (int jj = 0; jj < G8; jj++) {
+          const uint64_t p = blk + lo + (static_cast<uint64_t>(g0 + jj) << q.dlo_log);
+          if (__builtin_amdgcn_readlane(my, g0 + jj) >= 0) {  // wave-uniform
+            dev::xor_into(v[g0 + jj], t[jj]);
+            dev::mul_inplace(v[g0 + jj], dev::load_tab(st + p));
+          } else {
+            dev::zero(v[g0 + jj]);
+          }
+          if (act && p < rmax) stp(row_rsrc(y + p * sb), so, v[g0 + jj]);
+        }
+      }
+    } else if constexpr ((MODE & kEpOut) != 0) {
       uint8_t *par = a.parity + s * a.parity_stripe_stride + j * C * sb;
 #pragma unroll
       for (int jj = 0; jj < N; jj++) {
@@ -1156,6 +1202,68 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
       for (int jj = 0; jj < N; jj++) {
         const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
         if (act && p < n_dst) stp(row_rsrc(y + p * sb), so, v[jj]);
+      }
+    }
+  }
+}
+
+// The low-rate reconstruct in block form (launch_low_blocks): the final FFT's (skew 0) first
+// phase with block K's IFFT_{C, skew KC} last phase fused in (ifft_last_in), adding block K's
+// share of A' = F1(U' + V) and B' = F1(U) (U = D_C's argument, U' = (I + H) U as k_dphase's
+// DERIV, V the blocks' plain terms) to what the earlier blocks stored (acc): the block's
+// syndromes were scaled by sigma_K, so its U term is b (u = 1) or none (u = 0) and its V term
+// gamma b (the first block stores B' = 0 when it has no U term). k_dphase's LSUM then forms
+// A' + L B' = F1 (D_C U + V).
+template <int NI>
+__global__ __launch_bounds__(kBlock) void k_lbfinal(uint64_t n_stripes, PhaseArgs q, const RsTab *gamma, uint32_t u,
+                                                    uint32_t acc) {
+  constexpr int N = 64;
+  const uint64_t sb = q.sb, uu = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const bool act = uu < sb / 8;
+  const uint32_t so = act ? static_cast<uint32_t>(uu * 8) : 0u;
+  const uint64_t sub = blockIdx.y, dlo = 1ull << q.dlo_log;
+  const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
+  for (uint64_t s = blockIdx.z; s < n_stripes; s += gridDim.z) {
+    const uint8_t *x = q.src + s * q.src_stride;
+#pragma unroll 1
+    for (uint32_t pass = u || !acc ? 0u : 1u; pass < 2; pass++) {  // 0: B' (u = 0: zero, first block only), 1: A'
+      Sym<1> v[N];
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (p < q.n_src && (pass == 1 || u)) ldp(v[j], row_rsrc(x + p * sb), so);
+        else dev::zero(v[j]);
+      }
+      ifft_last_in<N, NI>(v, q);
+      if (pass == 1 && u) {  // v = (I + H) v + gamma v, ascending (reads above writes)
+        const Tab g = dev::load_tab(gamma);
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+          Sym<1> t = v[j];
+          dev::mul_inplace(t, g);
+#pragma unroll
+          for (int bb = 1; bb < N; bb <<= 1)
+            if (!(j & bb)) dev::xor_into(v[j], v[j + bb]);
+          dev::xor_into(v[j], t);
+        }
+      }
+      fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+      uint8_t *y = (pass == 0 ? q.dst2 : q.dst) + s * q.dst_stride;
+      if (acc) {
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+          const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+          if (p < q.n_dst) {
+            Sym<1> o;
+            ldp(o, row_rsrc(y + p * sb), so);
+            dev::xor_into(v[j], o);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
       }
     }
   }
@@ -2381,6 +2489,117 @@ static hipError_t launch_encode_low_phases(const EncodeArgs &a, hipStream_t s) {
                           : launch_ephase<kEpFft, 64>(fph[i].n, ni, g, b, q, subs, fc, s);
       if (e != hipSuccess) return e;
     }
+  }
+  return hipSuccess;
+}
+
+// per stripe: coefficients (C) | block K's transform (C) | A' and B' (the final FFT's first-phase
+// rows the later phases read)
+static uint64_t low_block_ylen(uint64_t C, uint64_t k) {
+  std::vector<XPhase> fph;
+  xform_phases(C, false, fph);
+  return round_up(k, 1ull << fph[0].dlo_log);
+}
+uint64_t low_block_rows(uint64_t C, uint64_t k) { return 2 * C + 2 * low_block_ylen(C, k); }
+
+static hipError_t launch_lbfinal(uint32_t ni, dim3 g, uint64_t n, const PhaseArgs &q, const RsTab *gamma, uint32_t u,
+                                 uint32_t acc, hipStream_t s) {
+  switch (ni) {
+#define RS_LBF_CASE(NI_) \
+  case NI_: hipLaunchKernelGGL((k_lbfinal<NI_>), g, dim3(kBlock), 0, s, n, q, gamma, u, acc); break;
+    RS_LBF_CASE(2) RS_LBF_CASE(4) RS_LBF_CASE(8) RS_LBF_CASE(16) RS_LBF_CASE(32) RS_LBF_CASE(64)
+#undef RS_LBF_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// rs_lowrate.cpp's block form as phase launches (scalar_reconstruct_low_blocks step by step):
+//  1. coefficients of d' = IFFT_C(originals, erased ones zero, trunc k): its phases but the last
+//     (k_ephase GATHER with a.skip), region 0;
+//  2. per block K = j + 1 holding rows used: FFT_{C, skew KC}(coefficients) (the IFFT's last
+//     phase fused into its first, as launch_encode_low_phases), its last phase forming the
+//     syndromes (SYN) into region 1; the IFFT_{C, skew KC} of those, in place, but its last
+//     phase, which runs inside k_lbfinal (the final FFT's first phase, accumulating A', B');
+//  3. the final FFT's later phases: LSUM (A' + L B', D_C's low bits) and SCATTER (the erased
+//     originals times exp(-L_g)) as launch_decode_generic's.
+hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
+  const EncodeArgs &a = L.enc;
+  const uint64_t C = a.chunk, sb = a.shard_bytes, k = a.k, mp = a.m;
+  if (C < 128 || (C & (C - 1)) || C > 32768 || sb % 64 || k == 0 || k > C || mp == 0 || a.n_chunks == 0 ||
+      mp > static_cast<uint64_t>(a.n_chunks) * C)
+    return hipErrorInvalidValue;
+  std::vector<XPhase> iph, fph;
+  xform_phases(C, true, iph);
+  xform_phases(C, false, fph);
+  if (iph.size() < 2 || fph.size() < 2 || fph.size() > 3 || fph[0].n != 64 ||
+      (64u >> (iph.back().dlo_log - fph[0].dlo_log)) != iph.back().n || (64ull << fph[0].dlo_log) != C)
+    return hipErrorInvalidValue;  // the shapes xform_phases gives every C in [128, 32768]
+  const uint64_t ylen = low_block_ylen(C, k), stride = low_block_rows(C, k) * sb;
+  uint8_t *X = a.scratch, *R1 = X + C * sb, *Ap = X + 2 * C * sb, *Bp = Ap + ylen * sb;
+  const bool contig = contig_ok(sb, 1);
+  const dim3 g0 = grid_for(sb, 1, 1);
+  const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
+  const uint64_t TI = ifft_tab_count(C);
+  uint64_t lim = 0;
+  for (size_t i = 0; i + 1 < iph.size(); i++) {  // 1.
+    const uint64_t span = static_cast<uint64_t>(iph[i].n) << iph[i].dlo_log, wl = round_up(k, span);
+    PhaseArgs q{X, X, stride, stride, i == 0 ? k : lim, wl, sb, C, k, iph[i].ti, a.tabs, iph[i].dlo_log, nullptr,
+                nullptr, contig, nullptr, 0, 0, 0};
+    const dim3 g(g0.x, static_cast<uint32_t>(wl / iph[i].n), gz);
+    hipError_t e = i == 0 ? launch_ephase<kEpGather, 64>(iph[i].n, 0, g, a, q, 0, 0, s)
+                          : launch_ephase<0, 64>(iph[i].n, 0, g, a, q, 0, 0, s);
+    if (e != hipSuccess) return e;
+    lim = wl;
+  }
+  for (uint32_t j = 0; j < a.n_chunks; j++) {  // 2.
+    EncodeArgs b = a;
+    b.chunk0 = j;
+    const uint64_t rj = std::min<uint64_t>(C, mp - static_cast<uint64_t>(j) * C);
+    for (size_t i = 0; i < fph.size(); i++) {
+      const bool first = i == 0, last = i + 1 == fph.size();
+      const uint32_t subs = static_cast<uint32_t>(C / fph[i].n);
+      PhaseArgs q{X, X, stride, stride, first ? lim : C, 0, sb, C, 0, fph[i].ti, a.tabs + TI, fph[i].dlo_log, nullptr,
+                  nullptr, contig, a.tabs, iph.back().ti, k, iph.back().dlo_log};
+      q.rec = L.rec;
+      q.rec_stride = L.rec_stripe_stride;
+      q.syn_idx = L.syn_idx;
+      q.syn_tab = L.syn_tab;
+      const dim3 g(g0.x, subs, gz);
+      hipError_t e = last ? launch_ephase<kEpFft | kEpSyn, 126>(fph[i].n, 0, g, b, q, subs, 1, s)
+                          : launch_ephase<kEpFft, 64>(fph[i].n, first ? iph.back().n : 0, g, b, q, subs, first ? 0 : 1, s);
+      if (e != hipSuccess) return e;
+    }
+    uint64_t lj = rj;  // rows of region 1 the next phase reads (the rest are zero)
+    const RsTab *ti = L.tabs_i + static_cast<uint64_t>(j) * TI;
+    for (size_t i = 0; i + 1 < iph.size(); i++) {
+      const uint64_t span = static_cast<uint64_t>(iph[i].n) << iph[i].dlo_log, wl = round_up(rj, span);
+      PhaseArgs q{R1, R1, stride, stride, lj, wl, sb, C, rj, iph[i].ti, ti, iph[i].dlo_log, nullptr, nullptr, contig,
+                  nullptr, 0, 0, 0};
+      const dim3 g(g0.x, static_cast<uint32_t>(wl / iph[i].n), gz);
+      hipError_t e = launch_ephase<0, 64>(iph[i].n, 0, g, b, q, 0, 0, s);
+      if (e != hipSuccess) return e;
+      lj = wl;
+    }
+    PhaseArgs q{R1, Ap, stride, stride, lj, ylen, sb, C, k, fph[0].ti, L.dec.tab_fft, fph[0].dlo_log, nullptr, Bp, contig,
+                ti, iph.back().ti, rj, iph.back().dlo_log};
+    const dim3 g(g0.x, static_cast<uint32_t>(C / 64), gz);
+    hipError_t e = launch_lbfinal(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s);
+    if (e != hipSuccess) return e;
+  }
+  DecodeArgs d = L.dec;  // 3.
+  d.n_stripes = a.n_stripes;
+  d.pattern_stride = 0;
+  for (size_t i = 1; i < fph.size(); i++) {
+    const bool last = i + 1 == fph.size();
+    const uint64_t span = static_cast<uint64_t>(fph[i].n) << fph[i].dlo_log, wl = round_up(k, span);
+    PhaseArgs q{Ap, Ap, stride, stride, ylen, ylen, sb, C, k, fph[i].ti, L.dec.tab_fft, fph[i].dlo_log, Bp, Bp, contig,
+                nullptr, 0, 0, 0};
+    const dim3 g(g0.x, static_cast<uint32_t>(wl / fph[i].n), gz);
+    hipError_t e = i == 1 ? (last ? launch_dphase<false, kPhLsum | kPhScatter, 126>(fph[i].n, g, d, q, s)
+                                  : launch_dphase<false, kPhLsum, 64>(fph[i].n, g, d, q, s))
+                          : launch_dphase<false, kPhScatter, 30>(fph[i].n, g, d, q, s);
+    if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }

@@ -42,6 +42,12 @@ struct LowDecodePlan {
   size_t off_fft = 0;
   uint32_t W = 0, trunc = 0, e = 0;
   std::shared_ptr<NetSlot> net;  // the pattern's reconstruct map (small codes)
+  // the block form (launch_low_blocks), when block_ok: one device blob at the off_* offsets
+  bool block = false;
+  uint32_t C = 0, n_blocks = 0, mprime = 0;
+  std::vector<uint8_t> u;
+  std::shared_ptr<DevBuf> bbuf;
+  size_t off_i = 0, off_f = 0, off_gamma = 0, off_syn = 0, off_post = 0, off_sidx = 0, off_dst = 0, off_skip = 0;
 };
 
 PlanCache<LowEncodePlan> g_low_enc;
@@ -168,6 +174,88 @@ int get_low_encode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, std::share
   return RS_OK;
 }
 
+// the block form: C-point transforms only (C >= 128: launch_low_blocks' phase shapes), any
+// number of blocks up to kLowBlockMaxBlocks; RS_AMD_LOW_BLOCK=0 keeps the W-point decode
+bool block_ok(uint64_t k, uint64_t m, uint64_t sb) {
+  const char *ev = std::getenv("RS_AMD_LOW_BLOCK");
+  if (ev && std::strcmp(ev, "0") == 0) return false;
+  const uint64_t C = ceil_pow2(k), W = ceil_pow2(C + m);
+  return C >= 128 && W / C <= kLowBlockMaxBlocks && sb % 64 == 0;
+}
+
+uint16_t log_of(uint16_t x) { return tables().log[x]; }
+
+// the device blob of the block form (layout: LowDecodePlan::off_*)
+int build_block_plan(int dev, uint64_t k, uint64_t m, const uint8_t *received, const uint16_t *er, LowDecodePlan &p) {
+  const uint64_t C = ceil_pow2(k);
+  uint64_t mp = 0;  // the last recovery row used + 1
+  for (uint64_t r = 0; r < m; r++)
+    if (received[C + r]) mp = r + 1;
+  if (mp == 0) return RS_OK;  // nothing erased: no block form needed
+  const uint64_t nbk = (mp + C - 1) / C;
+  std::vector<uint16_t> alpha, beta;
+  low_block_coefs(k, m, alpha, beta);
+  std::vector<RsTab> tabs;
+  push_ifft_tabs(tabs, C, 0, false);  // the low-rate encode's tables (launch_encode_low_phases)
+  for (uint64_t j = 0; j < nbk; j++) push_fft_tabs(tabs, C, (j + 1) * C, false);
+  const size_t n_e = tabs.size();
+  for (uint64_t j = 0; j < nbk; j++) push_ifft_tabs(tabs, C, (j + 1) * C, false);
+  const size_t n_i = tabs.size() - n_e;
+  push_fft_tabs(tabs, C, 0, false);
+  const size_t n_f = tabs.size() - n_e - n_i;
+  uint16_t zimg[16] = {};
+  const RsTab zero = make_tab_from_images(zimg);
+  p.u.assign(nbk, 0);
+  std::vector<uint16_t> sig(nbk, 0);
+  for (uint64_t j = 0; j < nbk; j++) {  // gamma: sigma_K = alpha_K (u = 1) or beta_K (u = 0)
+    const uint16_t al = alpha[j + 1], be = beta[j + 1];
+    if (al) {
+      p.u[j] = 1;
+      sig[j] = al;
+      tabs.push_back(be ? make_tab(static_cast<uint16_t>((log_of(be) + kModulus - log_of(al)) % kModulus), false) : zero);
+    } else {
+      sig[j] = be;  // both zero: the block adds nothing (its syndromes are scaled to zero)
+      tabs.push_back(make_tab(0, false));
+    }
+  }
+  std::vector<int32_t> sidx(nbk * C, -1), dst(C, -1);
+  const size_t at_syn = tabs.size();
+  tabs.resize(at_syn + nbk * C + C, zero);
+  for (uint64_t r = 0; r < mp; r++)
+    if (received[C + r]) {
+      sidx[r] = 1;
+      const uint16_t sg = sig[r / C];
+      tabs[at_syn + r] = sg ? make_tab(static_cast<uint16_t>((er[C + r] + log_of(sg)) % kModulus), false) : zero;
+    }
+  int32_t ne = 0;
+  std::vector<uint32_t> skip((k + 31) / 32, 0);
+  for (uint64_t g = 0; g < k; g++)
+    if (!received[g]) {
+      dst[g] = ne++;
+      tabs[at_syn + nbk * C + g] = make_tab(static_cast<uint16_t>(kModulus - er[g]), false);
+      skip[g / 32] |= 1u << (g % 32);
+    }
+  p.off_i = n_e * sizeof(RsTab);
+  p.off_f = (n_e + n_i) * sizeof(RsTab);
+  p.off_gamma = (n_e + n_i + n_f) * sizeof(RsTab);
+  p.off_syn = at_syn * sizeof(RsTab);
+  p.off_post = (at_syn + nbk * C) * sizeof(RsTab);
+  p.off_sidx = tabs.size() * sizeof(RsTab);
+  p.off_dst = p.off_sidx + sidx.size() * sizeof(int32_t);
+  p.off_skip = p.off_dst + dst.size() * sizeof(int32_t);
+  std::vector<uint8_t> blob(p.off_skip + skip.size() * sizeof(uint32_t));
+  std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
+  std::memcpy(blob.data() + p.off_sidx, sidx.data(), sidx.size() * sizeof(int32_t));
+  std::memcpy(blob.data() + p.off_dst, dst.data(), dst.size() * sizeof(int32_t));
+  std::memcpy(blob.data() + p.off_skip, skip.data(), skip.size() * sizeof(uint32_t));
+  if (int st = upload(blob.data(), blob.size(), dev, p.bbuf)) return st;
+  p.block = true;
+  p.C = static_cast<uint32_t>(C);
+  p.n_blocks = static_cast<uint32_t>(nbk);
+  p.mprime = static_cast<uint32_t>(mp);
+  return RS_OK;
+}
+
 int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present,
                         std::shared_ptr<LowDecodePlan> &out) {
   uint64_t e = 0;
@@ -175,8 +263,10 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
   const bool net = map_net_ok(k, e, sb);
   const char *te = std::getenv("RS_AMD_LOW_TRIM");
   const bool trim = !(te && std::strcmp(te, "0") == 0);
+  const bool blk = trim && e > 0 && block_ok(k, m, sb);
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
-                    std::to_string(net) + "/" + std::to_string(jit::max_blocks()) + "/" + (trim ? "t/" : "a/");
+                    std::to_string(net) + "/" + std::to_string(jit::max_blocks()) + "/" + (trim ? "t/" : "a/") +
+                    (blk ? "b/" : "w/");
   key.reserve(key.size() + k + m);
   for (uint64_t i = 0; i < k + m; i++) key.push_back(present[i] ? '1' : '0');
   {
@@ -187,7 +277,6 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
   auto p = std::make_shared<LowDecodePlan>();
   const uint64_t C = ceil_pow2(k), end = C + m, W = ceil_pow2(end);
   p->W = static_cast<uint32_t>(W);
-  if (int st = twiddle_plan(dev, W, 0, p->tw, p->off_fft)) return st;
   // position layout of scalar_reconstruct_low: originals [0, k), recovery [C, C + m). Only
   // the first e present recovery rows are read (round 5): with the k - e present originals and
   // the known zeros [k, C) that is exactly C known positions, the dimension of the code, and
@@ -203,6 +292,12 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
   p->trunc = static_cast<uint32_t>(trim ? last : end);
   std::vector<uint16_t> er(kOrder);
   erasure_logs_low(received.data(), k, m, er.data());
+  if (blk) {  // the block form needs none of the W-point tables
+    if (int st = build_block_plan(dev, k, m, received.data(), er.data(), *p)) return st;
+  }
+  if (!p->block) {
+    if (int st = twiddle_plan(dev, W, 0, p->tw, p->off_fft)) return st;
+  }
   std::vector<RsTab> tabs(2 * W);  // pre, post
   std::vector<int32_t> idx(2 * W, -1);  // src, dst
   uint32_t ne = 0;
@@ -220,10 +315,12 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
     }
   }
   p->e = ne;
-  std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + idx.size() * sizeof(int32_t));
-  std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
-  std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), idx.data(), idx.size() * sizeof(int32_t));
-  if (int st = upload(blob.data(), blob.size(), dev, p->buf)) return st;
+  if (!p->block) {
+    std::vector<uint8_t> blob(tabs.size() * sizeof(RsTab) + idx.size() * sizeof(int32_t));
+    std::memcpy(blob.data(), tabs.data(), tabs.size() * sizeof(RsTab));
+    std::memcpy(blob.data() + tabs.size() * sizeof(RsTab), idx.data(), idx.size() * sizeof(int32_t));
+    if (int st = upload(blob.data(), blob.size(), dev, p->buf)) return st;
+  }
   if (net) {
     p->net = std::make_shared<NetSlot>();
     p->net->async = !jit::supports(static_cast<uint32_t>(k), static_cast<uint32_t>(e), sb);
@@ -308,6 +405,45 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
       HIP_TRY(jit::launch(*nk, orig, ostride, rec, rstride, out, outstride, sb, n, s));
       return RS_OK;
     }
+  if (p->block) {
+    const uint8_t *base = static_cast<const uint8_t *>(p->bbuf->p);
+    LowBlockArgs L{};
+    EncodeArgs &a = L.enc;
+    a.data = orig;
+    a.data_stripe_stride = ostride;
+    a.shard_bytes = sb;
+    a.tabs = reinterpret_cast<const RsTab *>(base);
+    a.chunk = p->C;
+    a.n_chunks = p->n_blocks;
+    a.tabs_per_chunk = static_cast<uint32_t>(fft_tab_count(p->C));
+    a.k = static_cast<uint32_t>(k);
+    a.m = p->mprime;
+    a.skip = reinterpret_cast<const uint32_t *>(base + p->off_skip);
+    DecodeArgs &d = L.dec;
+    d.out = out;
+    d.out_stripe_stride = outstride;
+    d.shard_bytes = sb;
+    d.tab_fft = reinterpret_cast<const RsTab *>(base + p->off_f);
+    d.tab_post = reinterpret_cast<const RsTab *>(base + p->off_post);
+    d.pos_dst = reinterpret_cast<const int32_t *>(base + p->off_dst);
+    d.contig = contig_ok(sb, 1);
+    L.rec = rec;
+    L.rec_stripe_stride = rstride;
+    L.syn_idx = reinterpret_cast<const int32_t *>(base + p->off_sidx);
+    L.syn_tab = reinterpret_cast<const RsTab *>(base + p->off_syn);
+    L.tabs_i = reinterpret_cast<const RsTab *>(base + p->off_i);
+    L.gamma = reinterpret_cast<const RsTab *>(base + p->off_gamma);
+    L.u = p->u.data();
+    return in_scratch_slices(n, low_block_rows(p->C, k) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
+      LowBlockArgs b = L;
+      b.enc.data += s0 * ostride;
+      b.rec += s0 * rstride;
+      b.dec.out += s0 * outstride;
+      b.enc.n_stripes = cnt;
+      b.enc.scratch = scratch;
+      return launch_low_blocks(b, s);
+    });
+  }
   const KernelChoice kc = choose_decode_w(p->W, sb, max_nv);
   const uint8_t *base = static_cast<const uint8_t *>(p->buf->p);
   const uint8_t *tw = static_cast<const uint8_t *>(p->tw->p);
@@ -465,6 +601,7 @@ const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb) {
 
 const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e) {
   if (map_net_ok(k, e, sb)) return net_name("reconstruct_low", k, e);
+  if (e > 0 && block_ok(k, m, sb)) return "low_blocks";
   return choose_decode_w(ceil_pow2(ceil_pow2(k) + m), sb, 4).name;
 }
 

@@ -99,7 +99,12 @@ def test_low_rate_limits(monkeypatch):
     assert R.encode_kernel_name(10, 20, 1 << 16) == "net_encode_low_i10_o20"
     # 256 blocks: a background-compiled network (the FFT-form kernel until it is ready)
     assert R.encode_kernel_name(16, 64, 1 << 16) == "net_encode_low_i16_o64"
+    # C >= 128: the block form (C-point transforms); RS_AMD_LOW_BLOCK=0 or C < 128: W points
+    assert R.reconstruct_kernel_name(1000, 4000, 4096, [0] * 10 + [1] * 4990) == "low_blocks"
+    assert R.reconstruct_kernel_name(100, 600, 4096, [0] * 100 + [1] * 600) == "low_blocks"
+    monkeypatch.setenv("RS_AMD_LOW_BLOCK", "0")
     assert R.reconstruct_kernel_name(1000, 4000, 4096, [0] * 10 + [1] * 4990) == "decode_generic_nv1"
+    monkeypatch.delenv("RS_AMD_LOW_BLOCK")
     assert R.reconstruct_kernel_name(3, 5, 4096, [0, 1, 1] + [1] * 5).startswith("net_reconstruct_low")
     assert R.patterns_kernel_name(300, 1000, 4096, 300) == "pattern_fft_low"  # per-stripe patterns too
     monkeypatch.setenv("RS_AMD_NET_ASYNC_BLOCKS", "0")
@@ -107,6 +112,7 @@ def test_low_rate_limits(monkeypatch):
     monkeypatch.setenv("RS_AMD_JIT", "0")
     assert R.encode_kernel_name(10, 20, 1 << 16) == "encode_low_reg_w16_nv1"
     assert R.reconstruct_kernel_name(3, 5, 4096, [0, 1, 1] + [1] * 5) == "decode_reg_w16_nv4"
+    assert R.reconstruct_kernel_name(40, 100, 4096, [0] * 10 + [1] * 130) == "decode_generic_nv1"  # C = 64
 
 
 # ----------------------------------------------------------------- GPU
@@ -226,6 +232,77 @@ def test_low_rate_large_codes(oracle, k, m, sb, n):
         R.reconstruct_batch_dev(k, m, present, d, par, out)
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), data[:, missing]), e
+
+
+def _low_roundtrip(oracle, k, m, sb, n, present, seed, check_encode=True):
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev)
+    par = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
+    R.encode_batch_dev(k, m, d, par)
+    torch.cuda.synchronize()
+    if check_encode:
+        st, exp = oracle.encode_low(k, m, data[0])
+        assert st == 0 and np.array_equal(par[0].cpu().numpy(), exp)
+    missing = [i for i in range(k) if not present[i]]
+    out = torch.zeros((n, len(missing), sb), dtype=torch.uint8, device=dev)
+    R.reconstruct_batch_dev(k, m, present, d, par, out)
+    torch.cuda.synchronize()
+    return np.array_equal(out.cpu().numpy(), data[:, missing])
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("form", ["1", "0"])
+@pytest.mark.parametrize("k,m,sb,n,case", [
+    (300, 1000, 4096, 2, "first"),      # C = 512: the rows used all in block 1
+    (300, 1000, 4096, 2, "spread"),     # the first 450 recovery rows lost: rows used in blocks 1 and 2
+    (100, 600, 2048, 3, "tail"),        # C = 128 (2-point last phases), rows used in the last block
+    (128, 1000, 192 * 4, 2, "all"),     # every original lost
+    (1000, 4000, 4096, 2, "one"),       # C = 1024, one original lost
+    (5000, 9000, 64, 1, "spread"),      # C = 8192: three-phase transforms (LSUM, then SCATTER)
+    (16384, 40000, 64, 1, "all"),       # C = 16384, W = 65536
+])
+def test_low_rate_block_form(oracle, monkeypatch, form, k, m, sb, n, case):
+    """The low-rate reconstruct in block form (rs_lowrate.cpp, C-point transforms: the
+    residual's syndromes, per-block IFFTs, the derivative split as k_dphase's) against the
+    W-point decode (form 0) on the same losses: the restored originals are the lost data
+    either way (an MDS code's reconstruct is unique). Parity unpinned, as every low-rate path."""
+    monkeypatch.setenv("RS_AMD_LOW_BLOCK", form)
+    monkeypatch.setenv("RS_AMD_JIT", "0")  # no reconstruct network for the small losses
+    rng = np.random.default_rng(k + m + len(case))
+    C = 1 << (k - 1).bit_length()
+    present = np.ones(k + m, np.uint8)
+    if case == "all":
+        present[:k] = 0
+        present[k:k + m // 3] = 0
+    elif case == "one":
+        present[int(rng.integers(0, k))] = 0
+    else:
+        e = min(k, 97)
+        present[rng.choice(k, size=e, replace=False)] = 0
+        if case == "spread":
+            present[k:k + C - e // 2] = 0
+        elif case == "tail":
+            present[k:k + m - e - 3] = 0
+    assert int(present.sum()) >= k
+    name = R.reconstruct_kernel_name(k, m, sb, list(present))
+    assert name == ("low_blocks" if form == "1" else "decode_generic_nv1"), name
+    assert _low_roundtrip(oracle, k, m, sb, n, present, seed=k * 3 + m, check_encode=k <= 1000)
+
+
+@pytest.mark.gpu
+@gpu
+def test_low_rate_block_form_many_blocks(oracle):
+    """C = 128, W = 65536 (512 blocks): every original lost and the first 60,000 recovery rows
+    too, so the rows used sit in blocks 469 and 470 (the launch walks 470 blocks)."""
+    k, m, sb = 128, 65408, 64
+    present = np.ones(k + m, np.uint8)
+    present[:k] = 0
+    present[k:k + 60000] = 0
+    assert R.reconstruct_kernel_name(k, m, sb, list(present)) == "low_blocks"
+    assert _low_roundtrip(oracle, k, m, sb, 1, present, seed=128, check_encode=False)
 
 
 @pytest.mark.gpu
