@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -634,10 +635,36 @@ __device__ __forceinline__ void st(uint8_t *p, const Sym<NV> &s) {
 // between buffers costs no copy pass.
 __device__ __forceinline__ uint32_t log2_u64(uint64_t x) { return 63u - static_cast<uint32_t>(__builtin_clzll(x)); }
 
-// Generic.zig:80-147 on one position set (ti: table index of the phase's first layer)
+// A butterfly group's three twiddle tables are 63 SGPRs: the scheduler hoisting the next
+// groups' scalar loads above the current group's butterflies spilled SGPRs into VGPR lanes
+// (round 5: 1,200-2,300 SGPR spills per 64-point phase kernel, 250+ VGPRs, one wave per SIMD).
+// A scheduling barrier after each group keeps one group's tables live at a time.
+__device__ __forceinline__ void group_fence() { __builtin_amdgcn_sched_barrier(0); }
+// Values the compiler cannot prove loop-invariant (see opq(PhaseArgs)): plus a zero that a
+// volatile SALU move produces in place, so nothing derived from them is hoisted out of the
+// loop that calls this. (A readfirstlane round trip did the same but read an SGPR copy the
+// compiler had made in VGPRs under a narrower EXEC: garbage table addresses in partial waves.)
+__device__ __forceinline__ uint32_t vzero() {
+  uint32_t z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+template <class T>
+__device__ __forceinline__ T *opq(T *p) {
+  return p + vzero();
+}
+__device__ __forceinline__ uint64_t opqu(uint64_t v) { return v + vzero(); }
+__device__ __forceinline__ uint32_t opqu(uint32_t v) { return v + vzero(); }
+
+// Generic.zig:80-147 on one position set (ti: table index of the phase's first layer). The
+// group table offsets derive from opaque copies of ti / blk / dlo_log: computed where each
+// group runs, not hoisted out of the callers' loops and held (spilled) across them.
 template <int N, int NV>
 __device__ __forceinline__ void ifft_sub(Sym<NV> *s, const RsTab *__restrict__ tabs, uint64_t ti, uint64_t size,
                                          uint64_t rmax, uint64_t blk, uint32_t dlo_log) {
+  ti = opqu(ti);
+  blk = opqu(blk);
+  dlo_log = opqu(dlo_log);
   int jd = 1;
 #pragma unroll
   for (int jd4 = 4; jd4 <= N; jd4 <<= 2) {
@@ -656,6 +683,7 @@ __device__ __forceinline__ void ifft_sub(Sym<NV> *s, const RsTab *__restrict__ t
           dev::ifft_bf(s[i + jd], s[i + 3 * jd], m02);
         }
       }
+      group_fence();
     }
     ti += 3 * (size >> lg4);
     jd = jd4;
@@ -671,6 +699,9 @@ __device__ __forceinline__ void ifft_sub(Sym<NV> *s, const RsTab *__restrict__ t
 template <int N, int NV>
 __device__ __forceinline__ void fft_sub(Sym<NV> *s, const RsTab *__restrict__ tabs, uint64_t ti, uint64_t size,
                                         uint64_t rmax, uint64_t blk, uint32_t dlo_log) {
+  ti = opqu(ti);
+  blk = opqu(blk);
+  dlo_log = opqu(dlo_log);
   int jd4 = N;
 #pragma unroll
   for (int jd = N >> 2; jd != 0; jd >>= 2) {
@@ -689,6 +720,7 @@ __device__ __forceinline__ void fft_sub(Sym<NV> *s, const RsTab *__restrict__ ta
           dev::fft_bf(s[i + 2 * jd], s[i + 3 * jd], m23);
         }
       }
+      group_fence();
     }
     ti += 3 * (size >> lg4);
     jd4 = jd;
@@ -701,6 +733,7 @@ __device__ __forceinline__ void fft_sub(Sym<NV> *s, const RsTab *__restrict__ ta
         const Tab t = dev::load_tab(tabs + ti + r / 2);
         dev::fft_bf(s[jr], s[jr + 1], t);
       }
+      group_fence();
     }
   }
 }
@@ -751,18 +784,22 @@ __device__ __forceinline__ void xform_phase(const XformIO &io, bool first, bool 
   for (uint64_t blk = 0; blk < size; blk += span) {
     if (!INV && blk >= n_dst) break;  // FFT: a block past the stored outputs feeds nothing later
     for (uint64_t lo = 0; lo < dlo; lo++) {
+      // opaque per sub-problem: the N row offsets (j << dlo_log) * ps and the group tables are
+      // computed where used instead of hoisted out of the walk and spilled (see opq)
+      const uint32_t dl = opqu(dlo_log);
+      const RsTab *tb = opq(tabs);
       Sym<NV> s[N];
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dlo_log);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dl);
         if (p < n_src) ldb(s[j], row_rsrc(src + p * sps), io.off);
         else dev::zero(s[j]);
       }
-      if constexpr (INV) ifft_sub<N, NV>(s, tabs, ti, size, rmax, blk, dlo_log);
-      else fft_sub<N, NV>(s, tabs, ti, size, rmax, blk, dlo_log);
+      if constexpr (INV) ifft_sub<N, NV>(s, tb, ti, size, rmax, blk, dl);
+      else fft_sub<N, NV>(s, tb, ti, size, rmax, blk, dl);
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dlo_log);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dl);
         if (p < n_dst) {
           if (sym) dev::store_sym(dst + p * dps, io.off, s[j], io.contig);
           else stb(row_rsrc(dst + p * dps), io.off, s[j]);
@@ -909,6 +946,19 @@ struct PhaseArgs {
   const RsTab *syn_tab = nullptr;
 };
 
+// Table pointers made opaque inside the stripe / pass loops: a group's table loads are then
+// issued where the group runs. Hoisted out of the loops (the tables do not depend on the
+// stripe), every group's tables stayed live across them, 21 SGPRs each: 1,200-2,300 SGPRs
+// spilled into VGPR lanes per 64-point phase kernel and 250+ VGPRs, one wave per SIMD (round 5).
+__device__ __forceinline__ PhaseArgs opq(const PhaseArgs &q) {
+  PhaseArgs r = q;
+  r.tabs = opq(r.tabs);
+  r.tabs_i = opq(r.tabs_i);
+  r.syn_tab = opq(r.syn_tab);
+  r.dlo_log = opqu(r.dlo_log);  // the row offsets (blk + lo + (j << dlo_log)) * sb likewise
+  return r;
+}
+
 // The IFFT's last phase inside the first FFT phase's sub-problem: that sub-problem (fixed
 // position bits below dlo_f, registers j over the bits above) is the union of G = N / NI of
 // the IFFT phase's sub-problems (bits below dlo_i = dlo_f + log2 G fixed): group g holds
@@ -922,7 +972,7 @@ __device__ __forceinline__ void ifft_last_in(Sym<1> *v, const PhaseArgs &q) {
       Sym<1> w[NI];
 #pragma unroll
       for (int t = 0; t < NI; t++) w[t] = v[g + t * G];
-      ifft_sub<NI, 1>(w, q.tabs_i, q.ti_i, q.size, q.rmax_i, 0, q.dlo_i);
+      ifft_sub<NI, 1>(w, opq(q.tabs_i), q.ti_i, q.size, q.rmax_i, 0, q.dlo_i);  // the groups share tables
 #pragma unroll
       for (int t = 0; t < NI; t++) v[g + t * G] = w[t];
     }
@@ -946,7 +996,8 @@ __device__ __forceinline__ void stp(__amdgpu_buffer_rsrc_t r, uint32_t o, const 
 }
 
 template <int N, bool INV, int MODE, int NI = 0>
-__global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
+__global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q0) {
+  const PhaseArgs &q = q0;
   // lane unit u (4 symbols of one shard column); lanes past the shard's last unit stay (the
   // lane reads below need every lane): they load at offset 0 and store nothing
   const uint64_t sb = q.sb, u = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -959,6 +1010,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
   const uint64_t sub = blockIdx.y, dlo = 1ull << q.dlo_log;
   const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
   for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    const PhaseArgs q = opq(q0);
     Sym<1> v[N];
     if constexpr ((MODE & kPhSplitB) != 0) {  // B = F1(X), the sub-problem without H: first,
       // since A is then written over X (in place: the lane reads its positions before it
@@ -973,9 +1025,10 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
       }
       ifft_last_in<N, NI>(v, q);
       fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+      const uint32_t dls = opqu(q.dlo_log);  // store offsets recomputed, not held across the transform
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dls);
         if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
       }
     }
@@ -1003,8 +1056,10 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 #pragma unroll
         for (int j = 0; j < N; j++) dev::pair_halves(v[j], true);
 #pragma unroll
-      for (int j = 0; j < N; j++)
+      for (int j = 0; j < N; j++) {
         if (srcs[j] >= 0) dev::mul_inplace(v[j], dev::load_tab(tab_pre + blk + lo + (static_cast<uint64_t>(j) << q.dlo_log)));
+        group_fence();
+      }
     } else if constexpr ((MODE & kPhLsum) != 0) {
       const uint8_t *A = q.src + s * q.src_stride, *B = q.src2 + s * q.src_stride;
 #pragma unroll
@@ -1045,9 +1100,10 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
       }
     } else {
       const uint8_t *x = q.src + s * q.src_stride;
+      const uint32_t dll = opqu(q.dlo_log);  // not the SPLITB loads' offsets, held across its FFT
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dll);
         if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
         else dev::zero(v[j]);
       }
@@ -1079,12 +1135,14 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
           __builtin_amdgcn_raw_buffer_store_b32(v[j].l[0], r, io, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b32(v[j].h[0], r, io_h, 0, 0);
         }
+        group_fence();
       }
     } else {
       uint8_t *y = q.dst + s * q.dst_stride;
+      const uint32_t dls = opqu(q.dlo_log);  // store offsets recomputed, not held across the transform
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dls);
         if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
       }
     }
@@ -1104,7 +1162,8 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q) {
 enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4, kEpSyn = 8 };
 
 template <int N, int MODE, int NI>
-__global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, uint32_t subs, uint32_t from_chunk) {
+__global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q0, uint32_t subs, uint32_t from_chunk) {
+  const PhaseArgs &q = q0;
   const uint64_t sb = q.sb, u = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool act = u < sb / 8;
   const uint32_t so = act ? static_cast<uint32_t>(u * 8) : 0u;
@@ -1112,15 +1171,17 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
   const uint32_t io_h = io + (q.contig ? 256u : 32u);
   constexpr bool kFft = (MODE & kEpFft) != 0;
   const uint64_t C = q.size, dlo = 1ull << q.dlo_log;
-  const uint32_t ch = kFft ? blockIdx.y / subs : 0u;  // chunk of this launch
-  const uint64_t sub = kFft ? blockIdx.y % subs : blockIdx.y;
+  const uint32_t sl = static_cast<uint32_t>(__builtin_ctz(subs | (1u << 31)));  // subs: a power of two
+  const uint32_t ch = kFft ? blockIdx.y >> sl : 0u;  // chunk of this launch (scalar shifts, not a VALU divide)
+  const uint64_t sub = kFft ? blockIdx.y & (subs - 1) : blockIdx.y;
   const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
   const uint64_t j = a.chunk0 + ch;  // recovery chunk
   const uint64_t rmax = kFft ? (a.m - j * C < C ? a.m - j * C : C) : q.rmax;
   if (kFft && blk >= rmax) return;  // wave-uniform: outputs past the chunk's truncation feed nothing
-  const RsTab *tabs = kFft ? q.tabs + j * a.tabs_per_chunk : q.tabs;
   const uint64_t n_dst = kFft ? (rmax + dlo - 1) / dlo * dlo : q.n_dst;  // what later phases read
   for (uint64_t s = blockIdx.z; s < a.n_stripes; s += gridDim.z) {
+    const PhaseArgs q = opq(q0);
+    const RsTab *tabs = kFft ? q.tabs + j * a.tabs_per_chunk : q.tabs;
     Sym<1> v[N];
     const uint8_t *x = q.src + s * q.src_stride + (from_chunk ? (1 + ch) * C * sb : 0);
     if constexpr ((MODE & kEpGather) != 0) {
@@ -1182,6 +1243,7 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
             dev::zero(v[g0 + jj]);
           }
           if (act && p < rmax) stp(row_rsrc(y + p * sb), so, v[g0 + jj]);
+          group_fence();
         }
       }
     } else if constexpr ((MODE & kEpOut) != 0) {
@@ -1198,9 +1260,10 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
       }
     } else {
       uint8_t *y = q.dst + s * q.dst_stride + (kFft ? (1 + ch) * C * sb : 0);
+      const uint32_t dls = opqu(q.dlo_log);  // store offsets recomputed, not held across the transform
 #pragma unroll
       for (int jj = 0; jj < N; jj++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << q.dlo_log);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << dls);
         if (act && p < n_dst) stp(row_rsrc(y + p * sb), so, v[jj]);
       }
     }
@@ -1214,9 +1277,12 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q, ui
 // syndromes were scaled by sigma_K, so its U term is b (u = 1) or none (u = 0) and its V term
 // gamma b (the first block stores B' = 0 when it has no U term). k_dphase's LSUM then forms
 // A' + L B' = F1 (D_C U + V).
-template <int NI>
-__global__ __launch_bounds__(kBlock) void k_lbfinal(uint64_t n_stripes, PhaseArgs q, const RsTab *gamma, uint32_t u,
+template <int NI, int PASS>
+__global__ __launch_bounds__(kBlock) void k_lbfinal(uint64_t n_stripes, PhaseArgs q0, const RsTab *gamma, uint32_t u,
                                                     uint32_t acc) {
+  // PASS 0: B' (u = 0: zeros, stored by the first block only); PASS 1: A' (one launch each:
+  // a pass loop kept both passes' addresses live, 250+ VGPRs)
+  const PhaseArgs &q = q0;
   constexpr int N = 64;
   const uint64_t sb = q.sb, uu = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool act = uu < sb / 8;
@@ -1224,47 +1290,46 @@ __global__ __launch_bounds__(kBlock) void k_lbfinal(uint64_t n_stripes, PhaseArg
   const uint64_t sub = blockIdx.y, dlo = 1ull << q.dlo_log;
   const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
   for (uint64_t s = blockIdx.z; s < n_stripes; s += gridDim.z) {
+    const PhaseArgs q = opq(q0);
     const uint8_t *x = q.src + s * q.src_stride;
-#pragma unroll 1
-    for (uint32_t pass = u || !acc ? 0u : 1u; pass < 2; pass++) {  // 0: B' (u = 0: zero, first block only), 1: A'
-      Sym<1> v[N];
+    Sym<1> v[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+      if (p < q.n_src && (PASS == 1 || u)) ldp(v[j], row_rsrc(x + p * sb), so);
+      else dev::zero(v[j]);
+    }
+    ifft_last_in<N, NI>(v, q);
+    if (PASS == 1 && u) {  // v = (I + H) v + gamma v, ascending (reads above writes)
+      const Tab g = dev::load_tab(opq(gamma));
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (p < q.n_src && (pass == 1 || u)) ldp(v[j], row_rsrc(x + p * sb), so);
-        else dev::zero(v[j]);
-      }
-      ifft_last_in<N, NI>(v, q);
-      if (pass == 1 && u) {  // v = (I + H) v + gamma v, ascending (reads above writes)
-        const Tab g = dev::load_tab(gamma);
+        Sym<1> t = v[j];
+        dev::mul_inplace(t, g);
 #pragma unroll
-        for (int j = 0; j < N; j++) {
-          Sym<1> t = v[j];
-          dev::mul_inplace(t, g);
-#pragma unroll
-          for (int bb = 1; bb < N; bb <<= 1)
-            if (!(j & bb)) dev::xor_into(v[j], v[j + bb]);
-          dev::xor_into(v[j], t);
-        }
+        for (int bb = 1; bb < N; bb <<= 1)
+          if (!(j & bb)) dev::xor_into(v[j], v[j + bb]);
+        dev::xor_into(v[j], t);
       }
-      fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
-      uint8_t *y = (pass == 0 ? q.dst2 : q.dst) + s * q.dst_stride;
-      if (acc) {
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-          const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-          if (p < q.n_dst) {
-            Sym<1> o;
-            ldp(o, row_rsrc(y + p * sb), so);
-            dev::xor_into(v[j], o);
-          }
-        }
-      }
+    }
+    fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+    uint8_t *y = (PASS == 0 ? q.dst2 : q.dst) + s * q.dst_stride;
+    const uint32_t dls = opqu(q.dlo_log);  // output offsets recomputed, not held across the transform
+    if (acc) {
 #pragma unroll
       for (int j = 0; j < N; j++) {
-        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
-        if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dls);
+        if (p < q.n_dst) {
+          Sym<1> o;
+          ldp(o, row_rsrc(y + p * sb), so);
+          dev::xor_into(v[j], o);
+        }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dls);
+      if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
     }
   }
 }
@@ -2126,8 +2191,9 @@ hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStr
   // 1,024 lane columns of 64: RS(1000,4000) 4 KiB x 64 2.78 -> 1.91 ms); with more, the walk's
   // fewer launches win (RS(300,1000) 1 MiB x 16 32.7 vs 41.7 ms, 64 KiB x 8 1.29 vs 1.35 ms;
   // profiles/r04/lowrate/encode_phases.log)
-  if (kc.variant == Variant::kGeneric && a.chunk >= 64 && a.n_stripes * (a.shard_bytes / 8) < 64ull * 1024)
-    return launch_encode_low_phases(a, s);
+  const char *ph = std::getenv("RS_AMD_LOW_ENC_PHASES");  // 1 / 0: force the phase launches / the walk
+  const bool phases = ph && *ph ? std::strcmp(ph, "1") == 0 : a.n_stripes * (a.shard_bytes / 8) < 64ull * 1024;
+  if (kc.variant == Variant::kGeneric && a.chunk >= 64 && phases) return launch_encode_low_phases(a, s);
   if (kc.variant == Variant::kGeneric) {
     // a.scratch: `regions` C-position regions per stripe (low_encode): the coefficients, then
     // one per recovery chunk of a launch; the chunks run in groups of regions - 1
@@ -2506,7 +2572,10 @@ static hipError_t launch_lbfinal(uint32_t ni, dim3 g, uint64_t n, const PhaseArg
                                  uint32_t acc, hipStream_t s) {
   switch (ni) {
 #define RS_LBF_CASE(NI_) \
-  case NI_: hipLaunchKernelGGL((k_lbfinal<NI_>), g, dim3(kBlock), 0, s, n, q, gamma, u, acc); break;
+  case NI_:                                                                                   \
+    if (u || !acc) hipLaunchKernelGGL((k_lbfinal<NI_, 0>), g, dim3(kBlock), 0, s, n, q, gamma, u, acc); \
+    hipLaunchKernelGGL((k_lbfinal<NI_, 1>), g, dim3(kBlock), 0, s, n, q, gamma, u, acc);               \
+    break;
     RS_LBF_CASE(2) RS_LBF_CASE(4) RS_LBF_CASE(8) RS_LBF_CASE(16) RS_LBF_CASE(32) RS_LBF_CASE(64)
 #undef RS_LBF_CASE
     default: return hipErrorInvalidValue;
