@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q0) {
 enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4, kEpSyn = 8 };
 
 template <int N, int MODE, int NI>
-__global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q0, uint32_t subs, uint32_t from_chunk) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_ephase(EncodeArgs a, PhaseArgs q0, uint32_t subs, uint32_t from_chunk) {
   const PhaseArgs &q = q0;
   const uint64_t sb = q.sb, u = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
   const bool act = u < sb / 8;
@@ -1278,7 +1278,7 @@ __global__ __launch_bounds__(kBlock) void k_ephase(EncodeArgs a, PhaseArgs q0, u
 // gamma b (the first block stores B' = 0 when it has no U term). k_dphase's LSUM then forms
 // A' + L B' = F1 (D_C U + V).
 template <int NI, int PASS>
-__global__ __launch_bounds__(kBlock) void k_lbfinal(uint64_t n_stripes, PhaseArgs q0, const RsTab *gamma, uint32_t u,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_lbfinal(uint64_t n_stripes, PhaseArgs q0, const RsTab *gamma, uint32_t u,
                                                     uint32_t acc) {
   // PASS 0: B' (u = 0: zeros, stored by the first block only); PASS 1: A' (one launch each:
   // a pass loop kept both passes' addresses live, 250+ VGPRs)
@@ -1310,6 +1310,7 @@ __global__ __launch_bounds__(kBlock) void k_lbfinal(uint64_t n_stripes, PhaseArg
         for (int bb = 1; bb < N; bb <<= 1)
           if (!(j & bb)) dev::xor_into(v[j], v[j + bb]);
         dev::xor_into(v[j], t);
+        group_fence();  // one product live at a time (all 64 scheduled first: 247 VGPRs)
       }
     }
     fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
@@ -2187,12 +2188,12 @@ static hipError_t launch_encode_low_phases(const EncodeArgs &a, hipStream_t s);
 
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s) {
   trace_launch(kc.name);
-  // phase launches where the per-lane column walk leaves the chip short of waves (fewer than
-  // 1,024 lane columns of 64: RS(1000,4000) 4 KiB x 64 2.78 -> 1.91 ms); with more, the walk's
-  // fewer launches win (RS(300,1000) 1 MiB x 16 32.7 vs 41.7 ms, 64 KiB x 8 1.29 vs 1.35 ms;
-  // profiles/r04/lowrate/encode_phases.log)
+  // phase launches for every generic low-rate encode since the phase kernels stopped spilling
+  // (round 5: RS(300,1000) 1 MiB x 16 33.1 -> 23.4 ms, 64 KiB x 8 1.25 -> 0.76 ms, RS(1000,4000)
+  // 4 KiB x 64 2.74 -> 1.47 ms; profiles/r05/lowrate/encph.log). Round 4 kept the per-lane column
+  // walk where it had enough waves (then 32.7 vs 41.7 ms at 1 MiB x 16).
   const char *ph = std::getenv("RS_AMD_LOW_ENC_PHASES");  // 1 / 0: force the phase launches / the walk
-  const bool phases = ph && *ph ? std::strcmp(ph, "1") == 0 : a.n_stripes * (a.shard_bytes / 8) < 64ull * 1024;
+  const bool phases = ph && *ph ? std::strcmp(ph, "1") == 0 : true;
   if (kc.variant == Variant::kGeneric && a.chunk >= 64 && phases) return launch_encode_low_phases(a, s);
   if (kc.variant == Variant::kGeneric) {
     // a.scratch: `regions` C-position regions per stripe (low_encode): the coefficients, then
