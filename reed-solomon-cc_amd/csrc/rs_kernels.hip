@@ -996,7 +996,7 @@ __device__ __forceinline__ void stp(__amdgpu_buffer_rsrc_t r, uint32_t o, const 
 }
 
 template <int N, bool INV, int MODE, int NI = 0>
-__global__ __launch_bounds__(kBlock) void k_dphase(DecodeArgs a, PhaseArgs q0) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_dphase(DecodeArgs a, PhaseArgs q0) {
   const PhaseArgs &q = q0;
   // lane unit u (4 symbols of one shard column); lanes past the shard's last unit stay (the
   // lane reads below need every lane): they load at offset 0 and store nothing
