@@ -1159,7 +1159,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 // SYN (the low-rate reconstruct in block form, launch_low_blocks): the last FFT phase of block
 // K = j + 1 forms the residual's syndromes instead of storing recovery rows, and the gather
 // reads the originals flagged in a.skip (the erased ones) as zero.
-enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4, kEpSyn = 8 };
+// DLO (an IFFT phase of 64 contiguous positions, launch_low_blocks): besides its output U, the
+// phase stores W = (I + D_lo) U to dst2, D_lo the formal derivative's terms over the bits the
+// phase holds (bits 0-5): the later IFFT phases act on higher bits with twiddles that do not
+// depend on these, so they commute with D_lo and k_lbfin1 gets D_lo of the final IFFT output
+// by running the last IFFT phase on W.
+enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4, kEpSyn = 8, kEpDlo = 16 };
 
 template <int N, int MODE, int NI>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_ephase(EncodeArgs a, PhaseArgs q0, uint32_t subs, uint32_t from_chunk) {
@@ -1266,6 +1271,102 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << dls);
         if (act && p < n_dst) stp(row_rsrc(y + p * sb), so, v[jj]);
       }
+      if constexpr ((MODE & kEpDlo) != 0) {  // W = (I + D_lo) U, ascending (reads above writes)
+#pragma unroll
+        for (int jj = 0; jj < N; jj++) {
+#pragma unroll
+          for (int bb = 1; bb < N; bb <<= 1)
+            if (!(jj & bb)) dev::xor_into(v[jj], v[jj + bb]);
+        }
+        uint8_t *w = q.dst2 + s * q.dst_stride;
+        const uint32_t dlw = opqu(q.dlo_log);
+#pragma unroll
+        for (int jj = 0; jj < N; jj++) {
+          const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << dlw);
+          if (act && p < n_dst) stp(row_rsrc(w + p * sb), so, v[jj]);
+        }
+      }
+    }
+  }
+}
+
+// The final FFT's first phase for the block form with the derivative applied whole before it
+// (IFFTs of two phases, C <= 4096): block K's U = IFFT_last(U_pre) and
+// IFFT_last(W) = U + D_lo U (W from k_ephase DLO) are formed in VGPRs, then
+// Z = gamma U + D_hi U + IFFT_last(W) = D_C U + gamma U (D_hi: the derivative's terms over the
+// bits the last IFFT phase holds, register bits >= G = N / NI of this sub-problem) for u = 1,
+// Z = U for u = 0, and A' += F1(Z) (acc: add to what an earlier block stored). The next phase
+// is then a plain FFT phase with the scatter: no B' and no LSUM.
+template <int NI>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_lbfin1(uint64_t n_stripes,
+                                                                                         PhaseArgs q0,
+                                                                                         const RsTab *gamma,
+                                                                                         uint32_t u, uint32_t acc) {
+  const PhaseArgs &q = q0;
+  constexpr int N = 64, G = N / NI;
+  const uint64_t sb = q.sb, uu = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  const bool act = uu < sb / 8;
+  const uint32_t so = act ? static_cast<uint32_t>(uu * 8) : 0u;
+  const uint64_t sub = blockIdx.y, dlo = 1ull << q.dlo_log;
+  const uint64_t blk = (sub >> q.dlo_log) * (static_cast<uint64_t>(N) << q.dlo_log), lo = sub & (dlo - 1);
+  for (uint64_t s = blockIdx.z; s < n_stripes; s += gridDim.z) {
+    const PhaseArgs q = opq(q0);
+    const uint8_t *x = q.src + s * q.src_stride;
+    Sym<1> v[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << q.dlo_log);
+      if (p < q.n_src) ldp(v[j], row_rsrc(x + p * sb), so);
+      else dev::zero(v[j]);
+    }
+    ifft_last_in<N, NI>(v, q);
+    if (u) {
+      const Tab g = dev::load_tab(opq(gamma));
+#pragma unroll
+      for (int j = 0; j < N; j++) {  // gamma U + D_hi U, ascending (reads above writes)
+        Sym<1> t = v[j];
+        dev::mul_inplace(t, g);
+#pragma unroll
+        for (int bb = G; bb < N; bb <<= 1)
+          if (!(j & bb)) dev::xor_into(t, v[j + bb]);
+        v[j] = t;
+        group_fence();
+      }
+      const uint8_t *wq = q.src2 + s * q.src_stride;
+      const uint32_t dlw = opqu(q.dlo_log);
+#pragma unroll
+      for (int gg = 0; gg < G; gg++) {  // + IFFT_last(W), one group of the last IFFT phase at a time
+        Sym<1> w[NI];
+#pragma unroll
+        for (int t = 0; t < NI; t++) {
+          const uint64_t p = blk + lo + (static_cast<uint64_t>(gg + t * G) << dlw);
+          if (p < q.n_src) ldp(w[t], row_rsrc(wq + p * sb), so);
+          else dev::zero(w[t]);
+        }
+        ifft_sub<NI, 1>(w, opq(q.tabs_i), q.ti_i, q.size, q.rmax_i, 0, q.dlo_i);
+#pragma unroll
+        for (int t = 0; t < NI; t++) dev::xor_into(v[gg + t * G], w[t]);
+        group_fence();  // one group's W rows live at a time
+      }
+    }
+    fft_sub<N, 1>(v, q.tabs, q.ti, q.size, q.rmax, blk, q.dlo_log);
+    uint8_t *y = q.dst + s * q.dst_stride;
+    const uint32_t dls = opqu(q.dlo_log);
+    if (acc) {
+#pragma unroll
+      for (int j = 0; j < N; j++) {
+        const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dls);
+        if (p < q.n_dst) {
+          Sym<1> o;
+          ldp(o, row_rsrc(y + p * sb), so);
+          dev::xor_into(v[j], o);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      const uint64_t p = blk + lo + (static_cast<uint64_t>(j) << dls);
+      if (act && p < q.n_dst) stp(row_rsrc(y + p * sb), so, v[j]);
     }
   }
 }
@@ -2567,7 +2668,20 @@ static uint64_t low_block_ylen(uint64_t C, uint64_t k) {
   xform_phases(C, false, fph);
   return round_up(k, 1ull << fph[0].dlo_log);
 }
-uint64_t low_block_rows(uint64_t C, uint64_t k) { return 2 * C + 2 * low_block_ylen(C, k); }
+// X (coefficients) | R1 (block K's transform) | W (its (I + D_lo) copy, two-phase IFFTs) | A' | B'
+uint64_t low_block_rows(uint64_t C, uint64_t k) { return 3 * C + 2 * low_block_ylen(C, k); }
+
+static hipError_t launch_lbfin1(uint32_t ni, dim3 g, uint64_t n, const PhaseArgs &q, const RsTab *gamma, uint32_t u,
+                                uint32_t acc, hipStream_t s) {
+  switch (ni) {
+#define RS_LB1_CASE(NI_) \
+  case NI_: hipLaunchKernelGGL((k_lbfin1<NI_>), g, dim3(kBlock), 0, s, n, q, gamma, u, acc); break;
+    RS_LB1_CASE(2) RS_LB1_CASE(4) RS_LB1_CASE(8) RS_LB1_CASE(16) RS_LB1_CASE(32) RS_LB1_CASE(64)
+#undef RS_LB1_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 static hipError_t launch_lbfinal(uint32_t ni, dim3 g, uint64_t n, const PhaseArgs &q, const RsTab *gamma, uint32_t u,
                                  uint32_t acc, hipStream_t s) {
@@ -2606,7 +2720,10 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
       (64u >> (iph.back().dlo_log - fph[0].dlo_log)) != iph.back().n || (64ull << fph[0].dlo_log) != C)
     return hipErrorInvalidValue;  // the shapes xform_phases gives every C in [128, 32768]
   const uint64_t ylen = low_block_ylen(C, k), stride = low_block_rows(C, k) * sb;
-  uint8_t *X = a.scratch, *R1 = X + C * sb, *Ap = X + 2 * C * sb, *Bp = Ap + ylen * sb;
+  uint8_t *X = a.scratch, *R1 = X + C * sb, *Wr = X + 2 * C * sb, *Ap = X + 3 * C * sb, *Bp = Ap + ylen * sb;
+  // two IFFT phases (C <= 4096): the derivative whole before the final FFT (k_ephase DLO +
+  // k_lbfin1), so the final FFT's second phase is plain; else the A' / B' split (k_lbfinal, LSUM)
+  const bool whole = iph.size() == 2 && fph.size() == 2 && iph[0].n == 64 && iph[0].dlo_log == 0;
   const bool contig = contig_ok(sb, 1);
   const dim3 g0 = grid_for(sb, 1, 1);
   const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));
@@ -2644,17 +2761,19 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
     const RsTab *ti = L.tabs_i + static_cast<uint64_t>(j) * TI;
     for (size_t i = 0; i + 1 < iph.size(); i++) {
       const uint64_t span = static_cast<uint64_t>(iph[i].n) << iph[i].dlo_log, wl = round_up(rj, span);
-      PhaseArgs q{R1, R1, stride, stride, lj, wl, sb, C, rj, iph[i].ti, ti, iph[i].dlo_log, nullptr, nullptr, contig,
-                  nullptr, 0, 0, 0};
+      PhaseArgs q{R1, R1, stride, stride, lj, wl, sb, C, rj, iph[i].ti, ti, iph[i].dlo_log, nullptr, whole ? Wr : nullptr,
+                  contig, nullptr, 0, 0, 0};
       const dim3 g(g0.x, static_cast<uint32_t>(wl / iph[i].n), gz);
-      hipError_t e = launch_ephase<0, 64>(iph[i].n, 0, g, b, q, 0, 0, s);
+      hipError_t e = whole ? launch_ephase<kEpDlo, 64>(iph[i].n, 0, g, b, q, 0, 0, s)
+                           : launch_ephase<0, 64>(iph[i].n, 0, g, b, q, 0, 0, s);
       if (e != hipSuccess) return e;
       lj = wl;
     }
-    PhaseArgs q{R1, Ap, stride, stride, lj, ylen, sb, C, k, fph[0].ti, L.dec.tab_fft, fph[0].dlo_log, nullptr, Bp, contig,
-                ti, iph.back().ti, rj, iph.back().dlo_log};
+    PhaseArgs q{R1, Ap, stride, stride, lj, ylen, sb, C, k, fph[0].ti, L.dec.tab_fft, fph[0].dlo_log, whole ? Wr : nullptr,
+                Bp, contig, ti, iph.back().ti, rj, iph.back().dlo_log};
     const dim3 g(g0.x, static_cast<uint32_t>(C / 64), gz);
-    hipError_t e = launch_lbfinal(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s);
+    hipError_t e = whole ? launch_lbfin1(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s)
+                         : launch_lbfinal(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s);
     if (e != hipSuccess) return e;
   }
   DecodeArgs d = L.dec;  // 3.
@@ -2666,9 +2785,10 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
     PhaseArgs q{Ap, Ap, stride, stride, ylen, ylen, sb, C, k, fph[i].ti, L.dec.tab_fft, fph[i].dlo_log, Bp, Bp, contig,
                 nullptr, 0, 0, 0};
     const dim3 g(g0.x, static_cast<uint32_t>(wl / fph[i].n), gz);
-    hipError_t e = i == 1 ? (last ? launch_dphase<false, kPhLsum | kPhScatter, 126>(fph[i].n, g, d, q, s)
-                                  : launch_dphase<false, kPhLsum, 64>(fph[i].n, g, d, q, s))
-                          : launch_dphase<false, kPhScatter, 30>(fph[i].n, g, d, q, s);
+    hipError_t e = whole  ? launch_dphase<false, kPhScatter, 126>(fph[i].n, g, d, q, s)
+                   : i == 1 ? (last ? launch_dphase<false, kPhLsum | kPhScatter, 126>(fph[i].n, g, d, q, s)
+                                    : launch_dphase<false, kPhLsum, 64>(fph[i].n, g, d, q, s))
+                            : launch_dphase<false, kPhScatter, 30>(fph[i].n, g, d, q, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -358,8 +358,11 @@ def model_low_blocks(k, m, data, rec, present):
     assert len(iph) >= 2 and 2 <= len(fph) <= 3 and fph[0][0] == 64 and (64 << fph[0][1]) == C
     assert (64 >> (iph[-1][1] - fph[0][1])) == iph[-1][0]
     ylen = round_up(k, 1 << fph[0][1])
-    X, R1, Ap, Bp = 0, C, 2 * C, 2 * C + ylen
-    S = Scratch(2 * C + 2 * ylen)
+    X, R1, Wr, Ap = 0, C, 2 * C, 3 * C
+    Bp = Ap + ylen
+    S = Scratch(3 * C + 2 * ylen)
+    # two IFFT phases: the derivative whole before the final FFT (k_ephase DLO + k_lbfin1)
+    whole = len(iph) == 2 and len(fph) == 2
     tabsE = ifft_tabs(C, 0)
     TI = len(tabsE)
     for j in range(nbk):
@@ -436,9 +439,47 @@ def model_low_blocks(k, m, data, rec, present):
                 for p, x in zip(ps, v):
                     if p < wl:
                         S.write(R1 + p, x, sub)
+                if whole:  # DLO: W = (I + D_lo) U over the phase's 64 positions, ascending
+                    for jj in range(n):
+                        bb = 1
+                        while bb < n:
+                            if not (jj & bb):
+                                v[jj] ^= v[jj + bb]
+                            bb <<= 1
+                    for p, x in zip(ps, v):
+                        if p < wl:
+                            S.write(Wr + p, x, sub)
             lj = wl
-        # k_lbfinal
         n0, dl0, ti0 = fph[0]
+        if whole:  # k_lbfin1
+            S.launch()
+            G = 64 // ni
+            for sub in range(C // 64):
+                blk, ps = positions(64, sub, dl0)
+                v = [S.read(R1 + p, sub) if p < lj else 0 for p in ps]
+                ifft_last_in(v, ni, tabsI, tii, C, rj, dli)
+                if P["u"][j]:
+                    for jj in range(64):  # gamma U + D_hi U, ascending
+                        t = gmul(v[jj], P["gamma"][j])
+                        bb = G
+                        while bb < 64:
+                            if not (jj & bb):
+                                t ^= v[jj + bb]
+                            bb <<= 1
+                        v[jj] = t
+                    for gg in range(G):  # + IFFT_last(W)
+                        w = [S.read(Wr + ps[gg + t * G], sub) if ps[gg + t * G] < lj else 0 for t in range(ni)]
+                        ifft_sub(w, tabsI, tii, C, rj, 0, dli)
+                        for t in range(ni):
+                            v[gg + t * G] ^= w[t]
+                fft_sub(v, tabsF, ti0, C, k, blk, dl0)
+                for jj, p in enumerate(ps):
+                    if p < ylen:
+                        if j > 0:
+                            v[jj] ^= S.read(Ap + p, sub)
+                        S.write(Ap + p, v[jj], sub)
+            continue
+        # k_lbfinal
         S.launch()
         for sub in range(C // 64):
             blk, ps = positions(64, sub, dl0)
@@ -471,7 +512,7 @@ def model_low_blocks(k, m, data, rec, present):
         for sub in range(wl // n):
             blk, ps = positions(n, sub, dl)
             lo = ps[0] - blk
-            if i == 1:  # LSUM: A' + L B'
+            if i == 1 and not whole:  # LSUM: A' + L B'
                 Bv = [S.read(Bp + p, sub) if p < ylen else 0 for p in ps]
                 v = []
                 for jj in range(n):
@@ -505,6 +546,7 @@ def model_low_blocks(k, m, data, rec, present):
 CASES = [
     (100, 600, "first"), (100, 600, "spread"), (100, 600, "tail"), (130, 300, "all"), (300, 1000, "first"),
     (300, 1000, "spread"), (200, 1000, "one"), (64 + 1, 200, "spread"),
+    (5000, 9000, "spread"),  # C = 8192: three-phase transforms, the A' / B' split and LSUM
 ]
 
 
