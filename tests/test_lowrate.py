@@ -294,6 +294,24 @@ def test_low_rate_block_form(oracle, monkeypatch, form, k, m, sb, n, case):
 
 @pytest.mark.gpu
 @gpu
+@pytest.mark.parametrize("form", ["1", "0"])
+@pytest.mark.parametrize("cap_mb", ["1", "64"])
+def test_low_rate_reconstruct_scratch_cap(oracle, monkeypatch, form, cap_mb):
+    """The generic low-rate reconstructs under the scratch cap: a stripe's scratch (block form
+    3C + 2 ylen rows, W-point decode W + ylen rows; RS(300,1000) 4 KiB: 8.4 / 9.2 MiB) above a
+    1 MiB cap still runs, one stripe per slice; 64 MiB takes all three at once."""
+    monkeypatch.setenv("RS_AMD_LOW_BLOCK", form)
+    monkeypatch.setenv("RS_AMD_SCRATCH_CAP_MB", cap_mb)
+    monkeypatch.setenv("RS_AMD_JIT", "0")
+    k, m, sb, n = 300, 1000, 4096, 3
+    present = np.ones(k + m, np.uint8)
+    present[np.arange(0, 300, 3)] = 0
+    present[k:k + 50] = 0
+    assert _low_roundtrip(oracle, k, m, sb, n, present, seed=int(cap_mb) + 7 * int(form), check_encode=True)
+
+
+@pytest.mark.gpu
+@gpu
 def test_low_rate_block_form_many_blocks(oracle):
     """C = 128, W = 65536 (512 blocks): every original lost and the first 60,000 recovery rows
     too, so the rows used sit in blocks 469 and 470 (the launch walks 470 blocks)."""
