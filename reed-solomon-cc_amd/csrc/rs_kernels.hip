@@ -2668,8 +2668,18 @@ static uint64_t low_block_ylen(uint64_t C, uint64_t k) {
   xform_phases(C, false, fph);
   return round_up(k, 1ull << fph[0].dlo_log);
 }
-// X (coefficients) | R1 (block K's transform) | W (its (I + D_lo) copy, two-phase IFFTs) | A' | B'
-uint64_t low_block_rows(uint64_t C, uint64_t k) { return 3 * C + 2 * low_block_ylen(C, k); }
+// the derivative applied whole (k_ephase DLO + k_lbfin1) where the IFFT has two phases
+static bool low_block_whole(uint64_t C) {
+  std::vector<XPhase> iph, fph;
+  xform_phases(C, true, iph);
+  xform_phases(C, false, fph);
+  return iph.size() == 2 && fph.size() == 2 && iph[0].n == 64 && iph[0].dlo_log == 0;
+}
+// per stripe: X (coefficients) | R1 (block K's transform) | then W (its (I + D_lo) copy) | A'
+// for the whole derivative, A' | B' for the split one
+uint64_t low_block_rows(uint64_t C, uint64_t k) {
+  return low_block_whole(C) ? 3 * C + low_block_ylen(C, k) : 2 * C + 2 * low_block_ylen(C, k);
+}
 
 static hipError_t launch_lbfin1(uint32_t ni, dim3 g, uint64_t n, const PhaseArgs &q, const RsTab *gamma, uint32_t u,
                                 uint32_t acc, hipStream_t s) {
@@ -2720,10 +2730,11 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
       (64u >> (iph.back().dlo_log - fph[0].dlo_log)) != iph.back().n || (64ull << fph[0].dlo_log) != C)
     return hipErrorInvalidValue;  // the shapes xform_phases gives every C in [128, 32768]
   const uint64_t ylen = low_block_ylen(C, k), stride = low_block_rows(C, k) * sb;
-  uint8_t *X = a.scratch, *R1 = X + C * sb, *Wr = X + 2 * C * sb, *Ap = X + 3 * C * sb, *Bp = Ap + ylen * sb;
   // two IFFT phases (C <= 4096): the derivative whole before the final FFT (k_ephase DLO +
   // k_lbfin1), so the final FFT's second phase is plain; else the A' / B' split (k_lbfinal, LSUM)
-  const bool whole = iph.size() == 2 && fph.size() == 2 && iph[0].n == 64 && iph[0].dlo_log == 0;
+  const bool whole = low_block_whole(C);
+  uint8_t *X = a.scratch, *R1 = X + C * sb, *Wr = whole ? X + 2 * C * sb : nullptr;
+  uint8_t *Ap = X + (whole ? 3 : 2) * C * sb, *Bp = whole ? nullptr : Ap + ylen * sb;
   const bool contig = contig_ok(sb, 1);
   const dim3 g0 = grid_for(sb, 1, 1);
   const uint32_t gz = static_cast<uint32_t>(std::min<uint64_t>(a.n_stripes, 65535));

@@ -358,11 +358,13 @@ def model_low_blocks(k, m, data, rec, present):
     assert len(iph) >= 2 and 2 <= len(fph) <= 3 and fph[0][0] == 64 and (64 << fph[0][1]) == C
     assert (64 >> (iph[-1][1] - fph[0][1])) == iph[-1][0]
     ylen = round_up(k, 1 << fph[0][1])
-    X, R1, Wr, Ap = 0, C, 2 * C, 3 * C
-    Bp = Ap + ylen
-    S = Scratch(3 * C + 2 * ylen)
-    # two IFFT phases: the derivative whole before the final FFT (k_ephase DLO + k_lbfin1)
+    # two IFFT phases: the derivative whole before the final FFT (k_ephase DLO + k_lbfin1);
+    # per stripe X | R1 | W | A' for it, X | R1 | A' | B' for the split (low_block_rows)
     whole = len(iph) == 2 and len(fph) == 2
+    X, R1 = 0, C
+    Wr, Ap = (2 * C, 3 * C) if whole else (None, 2 * C)
+    Bp = None if whole else Ap + ylen
+    S = Scratch(3 * C + ylen if whole else 2 * C + 2 * ylen)
     tabsE = ifft_tabs(C, 0)
     TI = len(tabsE)
     for j in range(nbk):
