@@ -635,10 +635,10 @@ __device__ __forceinline__ void st(uint8_t *p, const Sym<NV> &s) {
 // between buffers costs no copy pass.
 __device__ __forceinline__ uint32_t log2_u64(uint64_t x) { return 63u - static_cast<uint32_t>(__builtin_clzll(x)); }
 
-// A butterfly group's three twiddle tables are 63 SGPRs: the scheduler hoisting the next
-// groups' scalar loads above the current group's butterflies spilled SGPRs into VGPR lanes
-// (round 5: 1,200-2,300 SGPR spills per 64-point phase kernel, 250+ VGPRs, one wave per SIMD).
-// A scheduling barrier after each group keeps one group's tables live at a time.
+// A butterfly group's three twiddle tables are 63 SGPRs. A scheduling barrier after each group
+// keeps the scheduler from lifting the next groups' table loads above it; on its own it did not
+// change the phase kernels' SGPR spills (those came from loop-invariant hoisting, see opq), so
+// it is kept as the per-group boundary the opaque tables below rely on.
 __device__ __forceinline__ void group_fence() { __builtin_amdgcn_sched_barrier(0); }
 // Values the compiler cannot prove loop-invariant (see opq(PhaseArgs)): plus a zero that a
 // volatile SALU move produces in place, so nothing derived from them is hoisted out of the
