@@ -141,6 +141,7 @@ struct LowBlockArgs {
   const RsTab *syn_tab;
   const RsTab *tabs_i;
   const RsTab *gamma;
+  const RsTab *gamma1;  // 1 + gamma[j] (the whole-derivative scheme's W)
   const uint8_t *u;
 };
 uint64_t low_block_rows(uint64_t C, uint64_t k);

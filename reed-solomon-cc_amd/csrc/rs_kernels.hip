@@ -1160,10 +1160,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 // K = j + 1 forms the residual's syndromes instead of storing recovery rows, and the gather
 // reads the originals flagged in a.skip (the erased ones) as zero.
 // DLO (an IFFT phase of 64 contiguous positions, launch_low_blocks): besides its output U, the
-// phase stores W = (I + D_lo) U to dst2, D_lo the formal derivative's terms over the bits the
-// phase holds (bits 0-5): the later IFFT phases act on higher bits with twiddles that do not
-// depend on these, so they commute with D_lo and k_lbfin1 gets D_lo of the final IFFT output
-// by running the last IFFT phase on W.
+// phase stores W = ((1 + gamma) I + D_lo) U to dst2 (1 + gamma: the block's table at syn_tab),
+// D_lo the formal derivative's terms over the bits the phase holds (bits 0-5): the later IFFT
+// phases act on higher bits with twiddles that do not depend on these, so they commute with D_lo
+// and k_lbfin1 gets (1 + gamma) U + D_lo U of the final IFFT output by running the last IFFT
+// phase on W.
 enum : int { kEpGather = 1, kEpOut = 2, kEpFft = 4, kEpSyn = 8, kEpDlo = 16 };
 
 template <int N, int MODE, int NI>
@@ -1271,12 +1272,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
         const uint64_t p = blk + lo + (static_cast<uint64_t>(jj) << dls);
         if (act && p < n_dst) stp(row_rsrc(y + p * sb), so, v[jj]);
       }
-      if constexpr ((MODE & kEpDlo) != 0) {  // W = (I + D_lo) U, ascending (reads above writes)
+      if constexpr ((MODE & kEpDlo) != 0) {  // W = ((1 + gamma) I + D_lo) U, ascending (reads above writes)
+        const Tab g1 = dev::load_tab(q.syn_tab);
 #pragma unroll
         for (int jj = 0; jj < N; jj++) {
+          Sym<1> t = v[jj];
+          dev::mul_inplace(t, g1);
 #pragma unroll
           for (int bb = 1; bb < N; bb <<= 1)
-            if (!(jj & bb)) dev::xor_into(v[jj], v[jj + bb]);
+            if (!(jj & bb)) dev::xor_into(t, v[jj + bb]);
+          v[jj] = t;
+          group_fence();
         }
         uint8_t *w = q.dst2 + s * q.dst_stride;
         const uint32_t dlw = opqu(q.dlo_log);
@@ -1292,16 +1298,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 
 // The final FFT's first phase for the block form with the derivative applied whole before it
 // (IFFTs of two phases, C <= 4096): block K's U = IFFT_last(U_pre) and
-// IFFT_last(W) = U + D_lo U (W from k_ephase DLO) are formed in VGPRs, then
-// Z = gamma U + D_hi U + IFFT_last(W) = D_C U + gamma U (D_hi: the derivative's terms over the
-// bits the last IFFT phase holds, register bits >= G = N / NI of this sub-problem) for u = 1,
-// Z = U for u = 0, and A' += F1(Z) (acc: add to what an earlier block stored). The next phase
-// is then a plain FFT phase with the scatter: no B' and no LSUM.
+// IFFT_last(W) = (1 + gamma) U + D_lo U (W from k_ephase DLO) are formed in VGPRs, then
+// Z = D_hi U + IFFT_last(W) = D_C U + gamma U (D_hi: the derivative's terms over the bits the
+// last IFFT phase holds, register bits >= G = N / NI of this sub-problem) for u = 1, Z = U for
+// u = 0, and A' += F1(Z) (acc: add to what an earlier block stored). The next phase is then a
+// plain FFT phase with the scatter: no B' and no LSUM.
 template <int NI>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_lbfin1(uint64_t n_stripes,
-                                                                                         PhaseArgs q0,
-                                                                                         const RsTab *gamma,
-                                                                                         uint32_t u, uint32_t acc) {
+                                                                                         PhaseArgs q0, uint32_t u,
+                                                                                         uint32_t acc) {
   const PhaseArgs &q = q0;
   constexpr int N = 64, G = N / NI;
   const uint64_t sb = q.sb, uu = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -1321,16 +1326,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
     ifft_last_in<N, NI>(v, q);
     if (u) {
-      const Tab g = dev::load_tab(opq(gamma));
 #pragma unroll
-      for (int j = 0; j < N; j++) {  // gamma U + D_hi U, ascending (reads above writes)
-        Sym<1> t = v[j];
-        dev::mul_inplace(t, g);
+      for (int j = 0; j < N; j++) {  // D_hi U, ascending (reads above writes)
+        Sym<1> t;
+        dev::zero(t);
 #pragma unroll
         for (int bb = G; bb < N; bb <<= 1)
           if (!(j & bb)) dev::xor_into(t, v[j + bb]);
         v[j] = t;
-        group_fence();
       }
       const uint8_t *wq = q.src2 + s * q.src_stride;
       const uint32_t dlw = opqu(q.dlo_log);
@@ -2681,11 +2684,11 @@ uint64_t low_block_rows(uint64_t C, uint64_t k) {
   return low_block_whole(C) ? 3 * C + low_block_ylen(C, k) : 2 * C + 2 * low_block_ylen(C, k);
 }
 
-static hipError_t launch_lbfin1(uint32_t ni, dim3 g, uint64_t n, const PhaseArgs &q, const RsTab *gamma, uint32_t u,
-                                uint32_t acc, hipStream_t s) {
+static hipError_t launch_lbfin1(uint32_t ni, dim3 g, uint64_t n, const PhaseArgs &q, uint32_t u, uint32_t acc,
+                                hipStream_t s) {
   switch (ni) {
 #define RS_LB1_CASE(NI_) \
-  case NI_: hipLaunchKernelGGL((k_lbfin1<NI_>), g, dim3(kBlock), 0, s, n, q, gamma, u, acc); break;
+  case NI_: hipLaunchKernelGGL((k_lbfin1<NI_>), g, dim3(kBlock), 0, s, n, q, u, acc); break;
     RS_LB1_CASE(2) RS_LB1_CASE(4) RS_LB1_CASE(8) RS_LB1_CASE(16) RS_LB1_CASE(32) RS_LB1_CASE(64)
 #undef RS_LB1_CASE
     default: return hipErrorInvalidValue;
@@ -2774,6 +2777,7 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
       const uint64_t span = static_cast<uint64_t>(iph[i].n) << iph[i].dlo_log, wl = round_up(rj, span);
       PhaseArgs q{R1, R1, stride, stride, lj, wl, sb, C, rj, iph[i].ti, ti, iph[i].dlo_log, nullptr, whole ? Wr : nullptr,
                   contig, nullptr, 0, 0, 0};
+      q.syn_tab = L.gamma1 + j;  // DLO: 1 + gamma of block K
       const dim3 g(g0.x, static_cast<uint32_t>(wl / iph[i].n), gz);
       hipError_t e = whole ? launch_ephase<kEpDlo, 64>(iph[i].n, 0, g, b, q, 0, 0, s)
                            : launch_ephase<0, 64>(iph[i].n, 0, g, b, q, 0, 0, s);
@@ -2783,7 +2787,7 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
     PhaseArgs q{R1, Ap, stride, stride, lj, ylen, sb, C, k, fph[0].ti, L.dec.tab_fft, fph[0].dlo_log, whole ? Wr : nullptr,
                 Bp, contig, ti, iph.back().ti, rj, iph.back().dlo_log};
     const dim3 g(g0.x, static_cast<uint32_t>(C / 64), gz);
-    hipError_t e = whole ? launch_lbfin1(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s)
+    hipError_t e = whole ? launch_lbfin1(iph.back().n, g, a.n_stripes, q, L.u[j], j > 0 ? 1u : 0u, s)
                          : launch_lbfinal(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s);
     if (e != hipSuccess) return e;
   }

@@ -47,7 +47,8 @@ struct LowDecodePlan {
   uint32_t C = 0, n_blocks = 0, mprime = 0;
   std::vector<uint8_t> u;
   std::shared_ptr<DevBuf> bbuf;
-  size_t off_i = 0, off_f = 0, off_gamma = 0, off_syn = 0, off_post = 0, off_sidx = 0, off_dst = 0, off_skip = 0;
+  size_t off_i = 0, off_f = 0, off_gamma = 0, off_gamma1 = 0, off_syn = 0, off_post = 0, off_sidx = 0, off_dst = 0,
+         off_skip = 0;
 };
 
 PlanCache<LowEncodePlan> g_low_enc;
@@ -218,6 +219,12 @@ int build_block_plan(int dev, uint64_t k, uint64_t m, const uint8_t *received, c
       tabs.push_back(make_tab(0, false));
     }
   }
+  for (uint64_t j = 0; j < nbk; j++) {  // 1 + gamma (k_ephase DLO: W = ((1 + gamma) I + D_lo) U)
+    const uint16_t al = alpha[j + 1], be = beta[j + 1];
+    const uint16_t gv = al && be ? tables().exp[(log_of(be) + kModulus - log_of(al)) % kModulus] : 0;
+    const uint16_t g1 = static_cast<uint16_t>(1u ^ gv);
+    tabs.push_back(p.u[j] && g1 ? make_tab(log_of(g1), false) : zero);
+  }
   std::vector<int32_t> sidx(nbk * C, -1), dst(C, -1);
   const size_t at_syn = tabs.size();
   tabs.resize(at_syn + nbk * C + C, zero);
@@ -238,6 +245,7 @@ int build_block_plan(int dev, uint64_t k, uint64_t m, const uint8_t *received, c
   p.off_i = n_e * sizeof(RsTab);
   p.off_f = (n_e + n_i) * sizeof(RsTab);
   p.off_gamma = (n_e + n_i + n_f) * sizeof(RsTab);
+  p.off_gamma1 = p.off_gamma + nbk * sizeof(RsTab);
   p.off_syn = at_syn * sizeof(RsTab);
   p.off_post = (at_syn + nbk * C) * sizeof(RsTab);
   p.off_sidx = tabs.size() * sizeof(RsTab);
@@ -433,6 +441,7 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
     L.syn_tab = reinterpret_cast<const RsTab *>(base + p->off_syn);
     L.tabs_i = reinterpret_cast<const RsTab *>(base + p->off_i);
     L.gamma = reinterpret_cast<const RsTab *>(base + p->off_gamma);
+    L.gamma1 = reinterpret_cast<const RsTab *>(base + p->off_gamma1);
     L.u = p->u.data();
     return in_scratch_slices(n, low_block_rows(p->C, k) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
       LowBlockArgs b = L;

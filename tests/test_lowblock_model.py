@@ -441,13 +441,16 @@ def model_low_blocks(k, m, data, rec, present):
                 for p, x in zip(ps, v):
                     if p < wl:
                         S.write(R1 + p, x, sub)
-                if whole:  # DLO: W = (I + D_lo) U over the phase's 64 positions, ascending
+                if whole:  # DLO: W = ((1 + gamma) I + D_lo) U over the phase's 64 positions, ascending
+                    g1 = (1 ^ P["gamma"][j]) if P["u"][j] else 0
                     for jj in range(n):
+                        t = gmul(v[jj], g1)
                         bb = 1
                         while bb < n:
                             if not (jj & bb):
-                                v[jj] ^= v[jj + bb]
+                                t ^= v[jj + bb]
                             bb <<= 1
+                        v[jj] = t
                     for p, x in zip(ps, v):
                         if p < wl:
                             S.write(Wr + p, x, sub)
@@ -461,8 +464,8 @@ def model_low_blocks(k, m, data, rec, present):
                 v = [S.read(R1 + p, sub) if p < lj else 0 for p in ps]
                 ifft_last_in(v, ni, tabsI, tii, C, rj, dli)
                 if P["u"][j]:
-                    for jj in range(64):  # gamma U + D_hi U, ascending
-                        t = gmul(v[jj], P["gamma"][j])
+                    for jj in range(64):  # D_hi U, ascending
+                        t = 0
                         bb = G
                         while bb < 64:
                             if not (jj & bb):
