@@ -1304,7 +1304,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) voi
 // u = 0, and A' += F1(Z) (acc: add to what an earlier block stored). The next phase is then a
 // plain FFT phase with the scatter: no B' and no LSUM.
 template <int NI>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void k_lbfin1(uint64_t n_stripes,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void k_lbfin1(uint64_t n_stripes,
                                                                                          PhaseArgs q0, uint32_t u,
                                                                                          uint32_t acc) {
   const PhaseArgs &q = q0;
