@@ -143,6 +143,7 @@ struct LowBlockArgs {
   const RsTab *gamma;
   const RsTab *gamma1;  // 1 + gamma[j] (the whole-derivative scheme's W)
   const uint8_t *u;
+  const uint8_t *used;  // host, per block: some recovery row of block K = j + 1 is read (else skipped)
 };
 uint64_t low_block_rows(uint64_t C, uint64_t k);
 hipError_t launch_low_blocks(const LowBlockArgs &a, hipStream_t s);

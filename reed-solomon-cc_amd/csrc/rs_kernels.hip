@@ -2753,7 +2753,11 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
     if (e != hipSuccess) return e;
     lim = wl;
   }
-  for (uint32_t j = 0; j < a.n_chunks; j++) {  // 2.
+  // 2. only the blocks holding a row used: an empty block's syndromes are zero and so is its
+  // contribution (linear), so the first block run stores A' (B') and later ones accumulate
+  bool stored = false;
+  for (uint32_t j = 0; j < a.n_chunks; j++) {
+    if (L.used && !L.used[j]) continue;
     EncodeArgs b = a;
     b.chunk0 = j;
     const uint64_t rj = std::min<uint64_t>(C, mp - static_cast<uint64_t>(j) * C);
@@ -2787,10 +2791,12 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
     PhaseArgs q{R1, Ap, stride, stride, lj, ylen, sb, C, k, fph[0].ti, L.dec.tab_fft, fph[0].dlo_log, whole ? Wr : nullptr,
                 Bp, contig, ti, iph.back().ti, rj, iph.back().dlo_log};
     const dim3 g(g0.x, static_cast<uint32_t>(C / 64), gz);
-    hipError_t e = whole ? launch_lbfin1(iph.back().n, g, a.n_stripes, q, L.u[j], j > 0 ? 1u : 0u, s)
-                         : launch_lbfinal(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], j > 0 ? 1u : 0u, s);
+    hipError_t e = whole ? launch_lbfin1(iph.back().n, g, a.n_stripes, q, L.u[j], stored ? 1u : 0u, s)
+                         : launch_lbfinal(iph.back().n, g, a.n_stripes, q, L.gamma + j, L.u[j], stored ? 1u : 0u, s);
     if (e != hipSuccess) return e;
+    stored = true;
   }
+  if (!stored) return hipErrorInvalidValue;  // no row used: the plan never asks for the block form
   DecodeArgs d = L.dec;  // 3.
   d.n_stripes = a.n_stripes;
   d.pattern_stride = 0;

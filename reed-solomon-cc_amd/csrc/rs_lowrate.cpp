@@ -45,7 +45,7 @@ struct LowDecodePlan {
   // the block form (launch_low_blocks), when block_ok: one device blob at the off_* offsets
   bool block = false;
   uint32_t C = 0, n_blocks = 0, mprime = 0;
-  std::vector<uint8_t> u;
+  std::vector<uint8_t> u, used;  // per block: u (host scalar form), some recovery row read
   std::shared_ptr<DevBuf> bbuf;
   size_t off_i = 0, off_f = 0, off_gamma = 0, off_gamma1 = 0, off_syn = 0, off_post = 0, off_sidx = 0, off_dst = 0,
          off_skip = 0;
@@ -184,6 +184,16 @@ bool block_ok(uint64_t k, uint64_t m, uint64_t sb) {
   return C >= 128 && W / C <= kLowBlockMaxBlocks && sb % 64 == 0;
 }
 
+// the block form serves a pattern when its shapes fit (block_ok) and the rows read are
+// trimmed to the first e present (RS_AMD_LOW_TRIM); shared by get_low_decode_plan and the
+// kernel-name prediction. Its work grows with the blocks holding a row read only
+// (launch_low_blocks skips the others), at most ceil(m / C) < W / C of them, so it stays
+// below the W-point decode's transforms for every pattern.
+bool block_form(uint64_t k, uint64_t m, uint64_t sb, uint64_t e) {
+  const char *te = std::getenv("RS_AMD_LOW_TRIM");
+  return !(te && std::strcmp(te, "0") == 0) && e > 0 && block_ok(k, m, sb);
+}
+
 uint16_t log_of(uint16_t x) { return tables().log[x]; }
 
 // the device blob of the block form (layout: LowDecodePlan::off_*)
@@ -207,6 +217,9 @@ int build_block_plan(int dev, uint64_t k, uint64_t m, const uint8_t *received, c
   uint16_t zimg[16] = {};
   const RsTab zero = make_tab_from_images(zimg);
   p.u.assign(nbk, 0);
+  p.used.assign(nbk, 0);
+  for (uint64_t r = 0; r < mp; r++)
+    if (received[C + r]) p.used[r / C] = 1;
   std::vector<uint16_t> sig(nbk, 0);
   for (uint64_t j = 0; j < nbk; j++) {  // gamma: sigma_K = alpha_K (u = 1) or beta_K (u = 0)
     const uint16_t al = alpha[j + 1], be = beta[j + 1];
@@ -271,7 +284,7 @@ int get_low_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint
   const bool net = map_net_ok(k, e, sb);
   const char *te = std::getenv("RS_AMD_LOW_TRIM");
   const bool trim = !(te && std::strcmp(te, "0") == 0);
-  const bool blk = trim && e > 0 && block_ok(k, m, sb);
+  const bool blk = block_form(k, m, sb, e);
   std::string key = std::to_string(dev) + "/" + std::to_string(k) + "/" + std::to_string(m) + "/" +
                     std::to_string(net) + "/" + std::to_string(jit::max_blocks()) + "/" + (trim ? "t/" : "a/") +
                     (blk ? "b/" : "w/");
@@ -443,6 +456,7 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
     L.gamma = reinterpret_cast<const RsTab *>(base + p->off_gamma);
     L.gamma1 = reinterpret_cast<const RsTab *>(base + p->off_gamma1);
     L.u = p->u.data();
+    L.used = p->used.data();
     return in_scratch_slices(n, low_block_rows(p->C, k) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
       LowBlockArgs b = L;
       b.enc.data += s0 * ostride;
@@ -610,7 +624,7 @@ const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb) {
 
 const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e) {
   if (map_net_ok(k, e, sb)) return net_name("reconstruct_low", k, e);
-  if (e > 0 && block_ok(k, m, sb)) return "low_blocks";
+  if (block_form(k, m, sb, e)) return "low_blocks";  // get_low_decode_plan's predicate
   return choose_decode_w(ceil_pow2(ceil_pow2(k) + m), sb, 4).name;
 }
 

@@ -305,7 +305,11 @@ int get_decode_plan(int dev, uint64_t k, uint64_t m, uint64_t sb, uint32_t flags
     out = lite;  // not (yet) worth a compile, or already queued
     return RS_OK;
   }
-  const bool pdec_on = pdec_want && pdec_admit(dev, k, m, key);
+  // how == 1 (a call the fused kernels cannot serve, e.g. max_nv != 4) takes the same reuse
+  // gate: a pattern below RS_AMD_PDEC_AFTER uses spends none of the code's RS_AMD_PDEC_MAX
+  // budget on a kernel that call cannot launch
+  const bool pdec_on = pdec_want && (how != 1 || (lite && lite->uses.load() >= pdec_after())) &&
+                       pdec_admit(dev, k, m, key);
   if (lite && !full && !use_net && !use_net_async && !syn_wins && !pdec_on) {
     out = lite;
     return RS_OK;

@@ -298,8 +298,10 @@ def test_low_rate_block_form(oracle, monkeypatch, form, k, m, sb, n, case):
 @pytest.mark.parametrize("cap_mb", ["1", "64"])
 def test_low_rate_reconstruct_scratch_cap(oracle, monkeypatch, form, cap_mb):
     """The generic low-rate reconstructs under the scratch cap: a stripe's scratch (block form
-    3C + 2 ylen rows, W-point decode W + ylen rows; RS(300,1000) 4 KiB: 8.4 / 9.2 MiB) above a
-    1 MiB cap still runs, one stripe per slice; 64 MiB takes all three at once."""
+    3C + ylen rows with the whole derivative (two IFFT phases, C <= 4096), 2C + 2 ylen with the
+    split one (low_block_rows); W-point decode W + ylen rows; several MiB each for RS(300,1000)
+    4 KiB) above a 1 MiB cap still runs, one stripe per slice; 64 MiB takes all three
+    at once."""
     monkeypatch.setenv("RS_AMD_LOW_BLOCK", form)
     monkeypatch.setenv("RS_AMD_SCRATCH_CAP_MB", cap_mb)
     monkeypatch.setenv("RS_AMD_JIT", "0")
@@ -321,6 +323,27 @@ def test_low_rate_block_form_many_blocks(oracle):
     present[k:k + 60000] = 0
     assert R.reconstruct_kernel_name(k, m, sb, list(present)) == "low_blocks"
     assert _low_roundtrip(oracle, k, m, sb, 1, present, seed=128, check_encode=False)
+
+
+@pytest.mark.gpu
+@gpu
+def test_low_rate_block_form_skips_empty_blocks(oracle, monkeypatch):
+    """the block form launches only the blocks holding a recovery row read (an empty
+    block's syndromes are zero and so is what it adds): C = 128, rows read in blocks 3 and 9 only
+    (1-2 and 4-8 skipped; the first block run stores A', the second accumulates). With
+    RS_AMD_LOW_TRIM=0 (every present row read) the kernel name and the plan agree on the W-point
+    decode."""
+    monkeypatch.setenv("RS_AMD_JIT", "0")
+    k, m, sb = 128, 1900, 256
+    present = np.zeros(k + m, np.uint8)
+    present[k // 2:k] = 1                            # 64 originals lost
+    present[k + 2 * 128 + 5:k + 2 * 128 + 37] = 1    # 32 rows in block 3
+    present[k + 8 * 128 + 1:k + 8 * 128 + 33] = 1    # 32 rows in block 9
+    assert R.reconstruct_kernel_name(k, m, sb, list(present)) == "low_blocks"
+    assert _low_roundtrip(oracle, k, m, sb, 2, present, seed=5, check_encode=False)
+    monkeypatch.setenv("RS_AMD_LOW_TRIM", "0")
+    assert R.reconstruct_kernel_name(k, m, sb, list(present)) != "low_blocks"
+    assert _low_roundtrip(oracle, k, m, sb, 2, present, seed=6, check_encode=False)
 
 
 @pytest.mark.gpu
