@@ -370,6 +370,19 @@ unsigned long long *stamp_buffer(int dev) {
   return p;
 }
 
+// Spec::present: where a wave's rows of R are loaded (RS_AMD_PDEC_RLOAD): 0 at the start of its
+// syndrome branch (round 4), 1 at the start of its final-FFT A layers (in flight during them),
+// 2 before the final FFT's B layers (round 4's dbg bit 5), 3 half at 1, half at 0
+int rload_of() {
+  const int v = env_int("RS_AMD_PDEC_RLOAD", 0);
+  return v >= 0 && v <= 3 ? v : 0;
+}
+
+// unit walk (RS_AMD_FFT_WALK): 1 = blocked (workgroup b takes units [b per, (b + 1) per): a
+// stripe's 2 KiB column slices in order, each shard row streamed sequentially by one CU),
+// 0 = interleaved (units b, b + grid, ...: every CU on the same two stripes at once)
+int walk_of() { return env_int("RS_AMD_FFT_WALK", 0) ? 1 : 0; }
+
 // the transpose / basis masks in VGPRs (RS_AMD_FFT_VMASK, default on)
 int vmask_of() { return env_int("RS_AMD_FFT_VMASK", 1) ? 1 : 0; }
 
@@ -916,9 +929,20 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         << " = LDB(us" << r << " ? RR : RZ, uo, pd" << r << " * sbl), rb" << r << " = LDB(us" << r
         << " ? RR1 : RZ, uo1, pd" << r << " * sbl);\n";
   };
-  if (tail && spat && (dbg & 32)) {  // static, early rows of R (measured: spills; bit 5 of RS_AMD_FFT_DEBUG)
+  // Spec::present: a wave's rows of R (static), loaded where RS_AMD_PDEC_RLOAD says; r0..r1 of them
+  const int rload = spat ? ((dbg & 32) ? 2 : rload_of()) : 0;
+  auto emit_rows_R = [&](uint32_t w, uint32_t r0, uint32_t r1) {
+    for (uint32_t r = r0; r < r1; r++) {
+      const uint32_t p = P.posA(w, r);
+      if (p < s.m && inR[p])
+        o << "  ra" << r << " = LDB(RR, uo, " << p << "u * sbl); rb" << r << " = LDB(RR1, uo1, " << p << "u * sbl);\n";
+    }
+  };
+  if (tail && rload) {
     o << "  v4 ";
     for (uint32_t r = 0; r < 8; r++) o << "ra" << r << ", rb" << r << (r < 7 ? ", " : ";\n");
+  }
+  if (tail && rload == 2) {  // before the final FFT's B layers (round 4 measured: spills)
     bool firstw = true;
     for (uint32_t w = 0; w < NW; w++) {
       bool any = false;
@@ -926,11 +950,7 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       if (!any) continue;
       o << "  " << (firstw ? "if" : "else if") << " (w == " << w << "u) {\n";
       firstw = false;
-      for (uint32_t r = 0; r < 8; r++) {
-        const uint32_t p = P.posA(w, r);
-        if (p < s.m && inR[p])
-          o << "  ra" << r << " = LDB(RR, uo, " << p << "u * sbl); rb" << r << " = LDB(RR1, uo1, " << p << "u * sbl);\n";
-      }
+      emit_rows_R(w, 0, 8);
       o << "  }\n";
     }
   } else if (tail && !old_order && !spat) {
@@ -979,13 +999,20 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
   }
   o << bar() << "  }\n";
   g.ops = &g.st->ops_a;
-  bool first = true;
-  for (uint32_t w = 0; w < NW; w++) {
+  auto anyout_of = [&](uint32_t w) {
     bool anyout = false;
     for (uint32_t r = 0; r < 8; r++) anyout |= P.out_mode[P.posA(w, r)] != kOutNone;
-    if (!anyout) continue;
-    o << "  " << (first ? "if" : "else if") << " (w == " << w << "u) {\n";
-    first = false;
+    return anyout;
+  };
+  // a wave's A layers of the final FFT; the decode kernels keep Enc(d') rows p < m in registers
+  // for the tail (Spec::present: emitted inside the tail's per-wave branch, below, with the
+  // wave's rows of R in flight during them when RS_AMD_PDEC_RLOAD is 1 or 3)
+  auto final_A = [&](uint32_t w, std::vector<uint8_t> &zout) {
+    if (tail && (rload == 1 || rload == 3)) {  // this wave's rows of R, in flight during its A layers
+      emit_rows_R(w, 0, rload == 1 ? 8 : 4);
+      o << "  asm volatile(\"\" ::: \"memory\");\n  __builtin_amdgcn_sched_barrier(0);\n";
+    }
+    g.ops = &g.st->ops_a;
     bool z[8];
     for (uint32_t r = 0; r < 8; r++) {
       const uint32_t p = P.posA(w, r);
@@ -999,10 +1026,22 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
         g.butterfly(wname(rx), z[rx], wname(ry), z[ry], false, P.get_tw(b.log_m));
       }
     }
-    if (s.decode) {  // Enc(d') rows p < m stay in registers for the decode tail
+    zout.assign(z, z + 8);
+    if (s.decode)
       for (uint32_t r = 0; r < 8; r++)
         if (P.posA(w, r) < s.m && z[r])
           for (int i = 0; i < 8; i++) o << "  " << wname(r) << "_" << i << " = 0u;\n";
+  };
+  bool first = true;
+  for (uint32_t w = 0; w < NW && !(spat && tail); w++) {
+    if (!anyout_of(w)) continue;
+    o << "  " << (first ? "if" : "else if") << " (w == " << w << "u) {\n";
+    first = false;
+    std::vector<uint8_t> zv;
+    final_A(w, zv);
+    bool z[8];
+    for (uint32_t r = 0; r < 8; r++) z[r] = zv[r] != 0;
+    if (s.decode) {
       o << "  }\n";
       continue;
     }
@@ -1068,15 +1107,21 @@ std::string gen_source(const Spec &s, const std::string &name, Stats *stats) {
       for (uint32_t r = 0; r < 8; r++)
         if (!z[r]) liveB[P.regB(P.posA(w, r))] = 1;
     }
-    // syndromes times L_p, IFFT A layers (per wave), A -> B
+    // (the final FFT's A layers), syndromes times L_p, IFFT A layers (per wave), A -> B
     o << "  {\n  LQ();\n";
     for (uint32_t w = 0; w < NW; w++) {
       o << "  " << (w ? "else if" : "if") << " (w == " << w << "u) {\n";
-      if (!(dbg & 32))  // this wave's rows of R, in flight together
+      if (anyout_of(w)) {
+        std::vector<uint8_t> zv;
+        final_A(w, zv);
+        o << "  __builtin_amdgcn_sched_barrier(0);\n";
+      }
+      if (!rload)  // this wave's rows of R, in flight together
         for (uint32_t r = 0; r < 8; r++)
           if (!z0[w][r])
             o << "  const v4 ra" << r << " = LDB(RR, uo, " << P.posA(w, r) << "u * sbl), rb" << r << " = LDB(RR1, uo1, "
               << P.posA(w, r) << "u * sbl);\n";
+      if (rload == 3) emit_rows_R(w, 4, 8);
       bool z[8];
       for (uint32_t r = 0; r < 8; r++) {
         z[r] = z0[w][r];
@@ -1447,7 +1492,7 @@ bool supports_inverse(uint64_t k, uint64_t m, uint64_t shard_bytes) {
 
 std::string cache_key(const Spec &s) {
   // code-shape knobs are part of the key (read when the source is generated)
-  std::string k = "fft4:p" + std::to_string(prefetch_of(s)) + ":s" + std::to_string(sched_of()) + ":d" +
+  std::string k = "fft4:p" + std::to_string(prefetch_of(s)) + (s.decode && !s.present.empty() && rload_of() ? ":rl" + std::to_string(rload_of()) : "") + ":s" + std::to_string(sched_of()) + ":d" +
                   std::to_string(debug_of()) + ":g" + std::to_string(rmul_group()) + ":k" + std::to_string(vmask_of()) + ":" +
                   std::to_string(s.k) + ":" +
                   std::to_string(s.m) + ":" + std::to_string(s.flags) + ":" +
@@ -1591,6 +1636,7 @@ Stats stats(const Spec &s) {
 const jit::Kernel *get(const Spec &s, bool async, std::string &err, bool &pending) {
   Spec copy = s;
   copy.prefetch = prefetch_of(s);
+  copy.blocked = copy.blocked || walk_of();
   for (;;) {
     const std::string name = kernel_name(copy);
     const jit::Kernel *k =

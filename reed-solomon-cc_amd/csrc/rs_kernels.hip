@@ -2732,6 +2732,7 @@ hipError_t launch_low_blocks(const LowBlockArgs &L, hipStream_t s) {
   if (iph.size() < 2 || fph.size() < 2 || fph.size() > 3 || fph[0].n != 64 ||
       (64u >> (iph.back().dlo_log - fph[0].dlo_log)) != iph.back().n || (64ull << fph[0].dlo_log) != C)
     return hipErrorInvalidValue;  // the shapes xform_phases gives every C in [128, 32768]
+  trace_launch("low_blocks");
   const uint64_t ylen = low_block_ylen(C, k), stride = low_block_rows(C, k) * sb;
   // two IFFT phases (C <= 4096): the derivative whole before the final FFT (k_ephase DLO +
   // k_lbfin1), so the final FFT's second phase is plain; else the A' / B' split (k_lbfinal, LSUM)

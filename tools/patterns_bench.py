@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Per-stripe erasure patterns (rs_reconstruct_batch_dev_patterns): RS(10,4) 1 MiB,
-4 random erasures per stripe: syndrome network (auto) vs matrix vs FFT path (RS_AMD_PATTERNS)."""
+4 random erasures per stripe: syndrome network (auto) vs matrix vs FFT path (RS_AMD_PATTERNS).
+Each line names the kernels the timed call launched (rs_last_kernels): for codes where the
+requested paths coincide (W > 32: matrix and fft both run the generic per-stripe path), the
+`launched` field shows it."""
 import json
 import os
 import sys
@@ -50,13 +53,15 @@ for var, val in variants:
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / 10
+    launched = R.last_kernels()  # what served the call: the label, not the env value
     ok = True
     for s in range(0, n, max(1, n // 64)):
         miss = [i for i in range(k) if not present[s, i]][:max_e]
         ok &= bool(torch.equal(out[s, :len(miss)], data[s, miss]))
     e_mean = float(np.minimum((present[:, :k] == 0).sum(1), max_e).mean())
     alg = n * sb * (k + m - loss + e_mean)  # present shards read + restored written
-    print(json.dumps({"path": path, var: val, "stripes": n, "ms": round(ms, 3), "alg_TBps": round(alg / ms / 1e9, 3),
-                      "verified": ok}), flush=True)
+    print(json.dumps({"requested": path, var: val, "launched": launched, "stripes": n, "ms": round(ms, 3),
+                      "alg_TBps": round(alg / ms / 1e9, 3), "frac": round(alg / ms / 8e9, 4), "verified": ok}),
+          flush=True)
     if var != "RS_AMD_PATTERNS":
         del os.environ[var]
