@@ -207,12 +207,12 @@ const char *rs_patterns_kernel_name(uint64_t original_count, uint64_t recovery_c
  * kernel (few losses: the direct map, queued at the pattern's second call; RS_AMD_FDEC=0:
  * the e x e syndrome map), else the fused kernel with the pattern compiled in
  * (rs_fft_pdecode_*, k <= 256; RS(200,55): 8-16 s of hipRTC), queued at the pattern's
- * RS_AMD_PDEC_AFTER-th call (default 3). The pattern-compiled kernels are bounded: at most
+ * RS_AMD_PDEC_AFTER-th call (default 2). The pattern-compiled kernels are bounded: at most
  * RS_AMD_PDEC_MAX (default 32) patterns per code and device (later patterns keep the
  * pattern-as-data kernel), and none is queued while more than RS_AMD_PDEC_QUEUE (default 2)
  * jobs wait on the worker (a later call retries). The calls run the first form until the
  * steady-state kernel is loaded. rs_net_wait blocks until the worker is idle (no plan build
- * or compile queued or running): after three calls + rs_net_wait the next call runs the
+ * or compile queued or running): after two calls + rs_net_wait the next call runs the
  * pattern's steady-state kernel (rs_reconstruct_warm gets there at once). RS_AMD_JIT_SYNC=1
  * compiles in the calling thread instead. Returns RS_OK. */
 int rs_net_wait(void);

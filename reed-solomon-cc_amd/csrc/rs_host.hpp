@@ -329,7 +329,7 @@ constexpr uint64_t kPdecMaxK = 256;  // pattern-compiled fused reconstruct: code
 bool pdec_enabled();
 // Bounds on the per-pattern compiles (each 1-16 s of hipRTC on the one background worker, and
 // a module that is never unloaded): a pattern is compiled in on its RS_AMD_PDEC_AFTER-th use
-// (default 3; rs_reconstruct_warm at once), at most RS_AMD_PDEC_MAX patterns per code and
+// (default 2, round 6: tools/pattern_stream.py; rs_reconstruct_warm at once), at most RS_AMD_PDEC_MAX patterns per code and
 // device (default 32; later patterns keep the pattern-as-data kernel), and not while more
 // than RS_AMD_PDEC_QUEUE jobs (default 2) wait on the worker (a later use retries).
 uint32_t pdec_after();

@@ -78,7 +78,7 @@ int env_num(const char *name, int def, int lo) {
 }
 }  // namespace
 
-uint32_t pdec_after() { return static_cast<uint32_t>(env_num("RS_AMD_PDEC_AFTER", 3, 1)); }
+uint32_t pdec_after() { return static_cast<uint32_t>(env_num("RS_AMD_PDEC_AFTER", 2, 1)); }
 size_t pdec_queue() { return static_cast<size_t>(env_num("RS_AMD_PDEC_QUEUE", 2, 0)); }
 
 bool pdec_admit(int dev, uint64_t k, uint64_t m, const std::string &key) {

@@ -61,7 +61,7 @@ R.encode_batch_dev(k, m, d, p)
 lost = list(range(2, k, 3))[:m]
 present = [0 if i in lost else 1 for i in range(k)] + [1] * m
 out = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
-for _ in range(3):  # the third use queues the upgrade: full plan build, then the pdecode compile
+for _ in range(3):  # the second use queues the upgrade: full plan build, then the pdecode compile
     R.reconstruct_batch_dev(k, m, present, d, p, out)
 torch.cuda.synchronize()
 assert torch.equal(out, d[:, lost])

@@ -1,7 +1,7 @@
 """Which kernel a reconstruct actually launches (rs_last_kernels) and the warm-up recipes of
 include/reedsol.h / INTEGRATION.md: a wide-code pattern's first calls run the fused FFT
 reconstruct with the pattern as data (rs_fft_decode_*); its RS_AMD_PDEC_AFTER-th call (default
-3) queues the same kernel with the pattern compiled in (rs_fft_pdecode_*), and three calls +
+2) queues the same kernel with the pattern compiled in (rs_fft_pdecode_*), and two calls +
 rs_net_wait, or one rs_reconstruct_warm, bring the pattern to it: the next call launches it.
 Per-pattern compiles are bounded (RS_AMD_PDEC_MAX per code) and a pattern whose steady state
 is a direct network compiles only that network. RS_AMD_FDEC=0 keeps
@@ -84,29 +84,31 @@ def test_warm_reaches_pattern_kernel(c4_batch, monkeypatch):
 
 
 def test_reuse_threshold_then_pattern_kernel(c4_batch, monkeypatch):
-    """The INTEGRATION.md recipe without the warm call: a pattern used twice is not compiled in
-    (RS_AMD_PDEC_AFTER, default 3: a one-off or twice-seen pattern costs no hipRTC); its third
-    call queues the compile, rs_net_wait, then the pattern-compiled kernel."""
+    """The INTEGRATION.md recipe without the warm call, call for call: a pattern used once is not
+    compiled in (RS_AMD_PDEC_AFTER, default 2: a one-off pattern costs no hipRTC); its second
+    call (still the pattern as data) queues the compile, rs_net_wait, then the third call runs
+    the pattern-compiled kernel."""
     monkeypatch.delenv("RS_AMD_FDEC", raising=False)
     monkeypatch.delenv("RS_AMD_PDEC_AFTER", raising=False)
     lost, present = pattern(403)
     assert has(run(present, lost, c4_batch), "rs_fft_decode")
-    run(present, lost, c4_batch)
     R.net_wait()
-    ran = run(present, lost, c4_batch)  # third use: still the pattern as data, queues the compile
+    ran = run(present, lost, c4_batch)  # second use: still the pattern as data, queues the compile
     assert has(ran, "rs_fft_decode_k200_m55") and not has(ran, "rs_fft_pdecode"), ran
     R.net_wait()
     ran = run(present, lost, c4_batch)
     assert has(ran, "rs_fft_pdecode_k200_m55"), ran
 
 
-def test_pdec_after_two(c4_batch, monkeypatch):
-    """RS_AMD_PDEC_AFTER=2: the second call queues the compile (round-4 behaviour)."""
+def test_pdec_after_three(c4_batch, monkeypatch):
+    """RS_AMD_PDEC_AFTER=3 (round 5's default): two calls compile nothing, the third queues."""
     monkeypatch.delenv("RS_AMD_FDEC", raising=False)
-    monkeypatch.setenv("RS_AMD_PDEC_AFTER", "2")
+    monkeypatch.setenv("RS_AMD_PDEC_AFTER", "3")
     lost, present = pattern(413)
     run(present, lost, c4_batch)
     run(present, lost, c4_batch)
+    R.net_wait()
+    assert not has(run(present, lost, c4_batch), "rs_fft_pdecode")  # third call queues
     R.net_wait()
     assert has(run(present, lost, c4_batch), "rs_fft_pdecode_k200_m55")
 
