@@ -297,7 +297,7 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
 // rs_reconstruct_warm for a low-rate pattern: its plan, and its network compiled
 int low_warm(int dev, uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present);
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb);
-const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present, uint64_t e);
+const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e);
 int low_decode_map(uint64_t k, uint64_t m, uint32_t flags, const uint8_t *present, jit::NetSpec &ns);
 // the low-rate reconstruct in block form (rs_lowrate.cpp): the scalars alpha_K, beta_K of the
 // W / C blocks, and the form on one symbol per position (host check); codes with at most

@@ -130,11 +130,7 @@ struct XPhase {
   uint64_t ti;
 };
 void xform_phases(uint64_t size, bool inv, std::vector<XPhase> &out);
-// the low-rate encode with a column's C-point state on chip (k_encode_low_lds: C = 512, shards
-// of whole 512-byte columns, contiguous lane layout): no scratch, the originals read once per
-// recovery chunk and every recovery row written once
-bool encode_low_lds_ok(uint64_t C, uint64_t shard_bytes);
-hipError_t launch_encode_low_lds(const EncodeArgs &a, hipStream_t s);
+
 hipError_t launch_encode_low(const KernelChoice &kc, const EncodeArgs &a, hipStream_t s);
 
 // Low-rate reconstruct in block form (rs_lowrate.cpp, C = ceilPow2(k) >= 128): C-point
@@ -160,10 +156,7 @@ struct LowBlockArgs {
 };
 uint64_t low_block_rows(uint64_t C, uint64_t k);
 hipError_t launch_low_blocks(const LowBlockArgs &a, hipStream_t s);
-// the block form with the state on chip (rs_lowlds.hip k_rec_low_lds): C = 512, the rows used
-// all in block j + 1, whole 512-byte columns; no scratch
-bool rec_low_lds_ok(uint64_t C, uint64_t shard_bytes);
-hipError_t launch_rec_low_lds(const LowBlockArgs &a, uint32_t j, hipStream_t s);
+
 // reconstruct as an n_out x n_in matrix of GF(2)-linear maps (decode matrix + GF MAC)
 KernelChoice choose_decode_matrix(uint32_t n_out, uint64_t shard_bytes, int max_nv);
 constexpr uint32_t kMatrixMaxOut = 8;

@@ -391,12 +391,6 @@ int low_encode(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, const u
   a.k = static_cast<uint32_t>(k);
   a.m = static_cast<uint32_t>(m);
   a.contig = kc.variant != Variant::kGeneric && contig_ok(sb, kc.nv);
-  if (kc.variant == Variant::kGeneric && encode_low_lds_ok(p->C, sb)) {  // C = 512: on chip, no scratch
-    a.contig = true;
-    a.n_stripes = n;
-    HIP_TRY(launch_encode_low_lds(a, s));
-    return RS_OK;
-  }
   if (kc.variant != Variant::kGeneric) {
     a.n_stripes = n;
     HIP_TRY(launch_encode_low(kc, a, s));
@@ -433,10 +427,6 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
       return RS_OK;
     }
   if (p->block) {
-    uint32_t n_used = 0, ju = 0;
-    for (uint32_t j = 0; j < p->used.size(); j++)
-      if (p->used[j]) n_used++, ju = j;
-    const bool lds = n_used == 1 && rec_low_lds_ok(p->C, sb);  // on chip, no scratch (rs_lowlds.hip)
     const uint8_t *base = static_cast<const uint8_t *>(p->bbuf->p);
     LowBlockArgs L{};
     EncodeArgs &a = L.enc;
@@ -467,12 +457,6 @@ int low_reconstruct(int dev, uint64_t k, uint64_t m, uint64_t sb, uint64_t n, co
     L.gamma1 = reinterpret_cast<const RsTab *>(base + p->off_gamma1);
     L.u = p->u.data();
     L.used = p->used.data();
-    if (lds) {
-      L.enc.n_stripes = n;
-      L.enc.contig = true;
-      HIP_TRY(launch_rec_low_lds(L, ju, s));
-      return RS_OK;
-    }
     return in_scratch_slices(n, low_block_rows(p->C, k) * sb, s, [&](uint64_t s0, uint64_t cnt, uint8_t *scratch) {
       LowBlockArgs b = L;
       b.enc.data += s0 * ostride;
@@ -635,26 +619,12 @@ bool scalar_reconstruct_low_blocks(uint16_t *data, const uint16_t *par, const ui
 
 const char *low_encode_kernel_name(uint64_t k, uint64_t m, uint64_t sb) {
   if (map_net_ok(k, m, sb)) return net_name("encode_low", k, m);
-  const KernelChoice kc = choose_encode_low(ceil_pow2(k), sb, 4);
-  if (kc.variant == Variant::kGeneric && encode_low_lds_ok(ceil_pow2(k), sb)) return "encode_low_lds";
-  return kc.name;
+  return choose_encode_low(ceil_pow2(k), sb, 4).name;
 }
 
-const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, const uint8_t *present, uint64_t e) {
+const char *low_reconstruct_kernel_name(uint64_t k, uint64_t m, uint64_t sb, uint64_t e) {
   if (map_net_ok(k, e, sb)) return net_name("reconstruct_low", k, e);
-  if (block_form(k, m, sb, e)) {  // get_low_decode_plan's predicate; low_reconstruct's LDS test
-    const uint64_t C = ceil_pow2(k);
-    std::vector<uint8_t> used;
-    for (uint64_t r = 0, nr = 0; r < m && nr < e; r++)
-      if (present[k + r]) {
-        nr++;
-        if (used.size() <= r / C) used.resize(r / C + 1, 0);
-        used[r / C] = 1;
-      }
-    uint32_t n_used = 0;
-    for (uint8_t b : used) n_used += b;
-    return n_used == 1 && rec_low_lds_ok(C, sb) ? "reconstruct_low_lds" : "low_blocks";
-  }
+  if (block_form(k, m, sb, e)) return "low_blocks";  // get_low_decode_plan's predicate
   return choose_decode_w(ceil_pow2(ceil_pow2(k) + m), sb, 4).name;
 }
 

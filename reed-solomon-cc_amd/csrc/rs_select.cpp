@@ -164,7 +164,7 @@ const char *rs_reconstruct_kernel_name(uint64_t k, uint64_t m, size_t sb, const 
   uint64_t e = 0, have = 0;
   for (uint64_t i = 0; i < k; i++) e += present[i] ? 0 : 1;
   for (uint64_t i = 0; i < k + m; i++) have += present[i] ? 1 : 0;
-  if (is_low_rate(k, m)) return low_reconstruct_kernel_name(k, m, sb, present, e);
+  if (is_low_rate(k, m)) return low_reconstruct_kernel_name(k, m, sb, e);
   const std::string mode = decode_mode_env();
   if (e == k && have == m && (mode == "auto" || mode == "net") && fft_enabled() && fftnet::supports_inverse(k, m, sb))
     return net_name("fft_inverse", m, k);

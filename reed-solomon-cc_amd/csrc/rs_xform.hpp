@@ -1,5 +1,5 @@
 // rs_xform.hpp — the column transforms' device primitives shared by the precompiled kernels
-// (rs_kernels.hip: the phase kernels; rs_lowlds.hip: the LDS-resident low-rate kernels):
+// (rs_kernels.hip):
 // Generic.zig:15-147 on a register set of N positions (ifft_sub / fft_sub, wave-uniform
 // twiddle tables in SGPRs), the opaque-value helpers that keep table addresses from being
 // hoisted out of loops, and the buffer resources of shard rows.

@@ -11,8 +11,6 @@ generator block), and the erasure-locator decode's algebra in the low-rate layou
 (rs_lowrate_selftest) for every size class up to 65,536-point transforms."""
 import itertools
 
-import os
-
 import numpy as np
 import pytest
 
@@ -290,9 +288,7 @@ def test_low_rate_block_form(oracle, monkeypatch, form, k, m, sb, n, case):
             present[k:k + m - e - 3] = 0
     assert int(present.sum()) >= k
     name = R.reconstruct_kernel_name(k, m, sb, list(present))
-    # C = 512 on whole 512-byte columns with the rows read in one block: the block form on chip
-    lds = C == 512 and sb % 512 == 0 and case in ("first", "all") and os.environ.get("RS_AMD_LOW_LDS") != "0"
-    assert name == (("reconstruct_low_lds" if lds else "low_blocks") if form == "1" else "decode_generic_nv1"), name
+    assert name == ("low_blocks" if form == "1" else "decode_generic_nv1"), name
     assert _low_roundtrip(oracle, k, m, sb, n, present, seed=k * 3 + m, check_encode=k <= 1000)
 
 
@@ -314,54 +310,6 @@ def test_low_rate_reconstruct_scratch_cap(oracle, monkeypatch, form, cap_mb):
     present[np.arange(0, 300, 3)] = 0
     present[k:k + 50] = 0
     assert _low_roundtrip(oracle, k, m, sb, n, present, seed=int(cap_mb) + 7 * int(form), check_encode=True)
-
-
-@pytest.mark.gpu
-@gpu
-@pytest.mark.parametrize("lds", ["1", "0"])
-@pytest.mark.parametrize("k,m,sb,n,case", [
-    (300, 1000, 512, 3, "first"),       # C = 512, one 512-byte column per shard
-    (300, 1000, 65536, 2, "first"),
-    (512, 600, 1024, 2, "first"),       # k = C: no IFFT truncation; one recovery chunk + 88 rows
-    (260, 600, 2048, 2, "all"),         # every original lost: the rows read fill block 1 (u / gamma path)
-    (400, 1500, 4096, 2, "second"),     # the first 512 recovery rows lost: the rows read all in block 2
-    (300, 1000, 576, 2, "first"),       # not whole 512-byte columns: the scratch sequence
-])
-def test_low_rate_lds_paths(oracle, monkeypatch, lds, k, m, sb, n, case):
-    """The on-chip low-rate kernels (rs_lowlds.hip, C = 512): the encode against the oracle's
-    rso_encode_low on every stripe, the block-form reconstruct by round trip (the restored
-    originals are the lost data), each against RS_AMD_LOW_LDS=0 (phase launches / scratch
-    sequence). Parity unpinned, as every low-rate path."""
-    monkeypatch.setenv("RS_AMD_LOW_LDS", lds)
-    monkeypatch.setenv("RS_AMD_JIT", "0")
-    rng = np.random.default_rng(k + 7 * m + sb)
-    present = np.ones(k + m, np.uint8)
-    if case == "all":
-        present[:k] = 0
-    else:
-        present[rng.choice(k, size=min(k, 97), replace=False)] = 0
-        if case == "second":
-            present[k:k + 512] = 0
-    on_chip = lds == "1" and sb % 512 == 0
-    assert R.encode_kernel_name(k, m, sb) == ("encode_low_lds" if on_chip else "encode_low_generic_nv1")
-    assert R.reconstruct_kernel_name(k, m, sb, list(present)) == ("reconstruct_low_lds" if on_chip else "low_blocks")
-    dev = torch.device("cuda:0")
-    data = rng.integers(0, 256, (n, k, sb), dtype=np.uint8)
-    d = torch.from_numpy(data).to(dev)
-    par = torch.zeros((n, m, sb), dtype=torch.uint8, device=dev)
-    R.encode_batch_dev(k, m, d, par)
-    torch.cuda.synchronize()
-    got = par.cpu().numpy()
-    for s in range(n):
-        st, exp = oracle.encode_low(k, m, data[s])
-        assert st == 0 and np.array_equal(got[s], exp), s
-    missing = [i for i in range(k) if not present[i]]
-    out = torch.zeros((n, len(missing), sb), dtype=torch.uint8, device=dev)
-    R.reconstruct_batch_dev(k, m, present, d, par, out)
-    ran = R.last_kernels()
-    torch.cuda.synchronize()
-    assert ("reconstruct_low_lds" in ran) == on_chip, ran
-    assert np.array_equal(out.cpu().numpy(), data[:, missing])
 
 
 @pytest.mark.gpu
