@@ -16,3 +16,25 @@ for shp in "k=16 m=16 loss=16 max_e=16" "k=40 m=12 loss=12 max_e=12"; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof16 -o run -- python3 tools/patterns_bench.py 256 k=16 m=16 loss=16 max_e=16 sb=1048576 > $O/prof16.log 2>&1 || { tail -5 $O/prof16.log; exit 1; }
 find $O/prof16 -name '*kernel_stats.csv' -exec cut -d, -f1-8 {} \; | head -12
+# (4) SQ / SQC counters of the per-stripe RS(16,16) call, one --pmc pass per group
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT" \
+           "SQC_DCACHE_HITS SQC_DCACHE_MISSES"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$(pwd)/$O/sq$i" -o run -- \
+    python3 tools/patterns_bench.py 256 k=16 m=16 loss=16 max_e=16 sb=1048576 > $O/sq$i.log 2>&1 || { echo "group $i failed"; tail -5 $O/sq$i.log; exit 1; }
+done
+python3 - "$O" <<'PY'
+import csv, glob, collections, sys
+agg = collections.defaultdict(dict)
+for f in glob.glob(sys.argv[1] + "/sq*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"][:70]
+        agg[k].setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+for k, d in agg.items():
+    if "at::" in k or "rs_fft_decode" not in k: continue
+    print(k)
+    for c, v in sorted(d.items()):
+        print(f"   {c:28s} {sum(v)/len(v):.6g}  (n={len(v)})")
+PY
