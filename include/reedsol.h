@@ -245,6 +245,13 @@ int64_t rs_debug_fail_alloc(int64_t n);
  * pooled one-shot contexts; compiled kernels stay loaded), after any background plan build
  * finished. *pooled_contexts (optional) = one-shot contexts left in the pool (0). */
 int rs_debug_release_caches(uint64_t *pooled_contexts);
+/* Host erasure locators (root.zig:277-289, Generic.zig:200-215 evalPoly): the library sums a
+ * small erased set's log terms point by point instead of the two 65536-point transforms.
+ * Evaluates both for `received` (high rate: recovery at [0, m), originals at [C, C + k),
+ * C = ceilPow2(m); low != 0: rs_gf.hpp erasure_logs_low's layout) and returns the number of
+ * positions below ceilPow2(C + k) (low: ceilPow2(C + m)) where they differ mod 65535; -1 on
+ * invalid arguments. Host only, no device. */
+int64_t rs_debug_erasure_logs_check(uint64_t k, uint64_t m, const uint8_t *received, int low);
 /* Measurement builds of the FFT kernels (RS_AMD_FFT_DEBUG bit 6, rs_fftnet.cpp): every wave
  * of workgroup 0 stamps s_memtime around each barrier of its third unit; copies the current
  * device's 8 x 64 stamps (wave-major) to out[0, min(n, 512)). */

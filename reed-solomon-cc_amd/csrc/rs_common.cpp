@@ -392,6 +392,23 @@ int rs_debug_release_caches(uint64_t *pooled_contexts) {
   });
 }
 
+int64_t rs_debug_erasure_logs_check(uint64_t k, uint64_t m, const uint8_t *received, int low) {
+  if (!received || k == 0 || m == 0 || k + m > kOrder) return -1;
+  const uint64_t C = ceil_pow2(low ? k : m), end = C + (low ? m : k), W = ceil_pow2(end);
+  if (W > kOrder) return -1;
+  std::vector<uint16_t> a(kOrder), b(kOrder);
+  std::vector<uint8_t> rcv(received, received + end);
+  rcv.resize(W, 0);
+  set_erasure_logs_fwht(false);
+  (low ? erasure_logs_low : erasure_logs)(rcv.data(), k, m, a.data());
+  set_erasure_logs_fwht(true);
+  (low ? erasure_logs_low : erasure_logs)(rcv.data(), k, m, b.data());
+  set_erasure_logs_fwht(false);
+  int64_t bad = 0;
+  for (uint64_t i = 0; i < W; i++) bad += a[i] % kModulus != b[i] % kModulus;
+  return bad;
+}
+
 int rs_net_wait(void) {
   return guarded([&]() -> int {
     jit::wait_pending();

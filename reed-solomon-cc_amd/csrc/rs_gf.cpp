@@ -3,6 +3,7 @@
 #include "rs_gf.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -170,6 +171,38 @@ void scalar_fft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool q)
     for (uint64_t r = 0; r < trunc; r += 2) fft_bf_s(s[r], s[r + 1], sk[r + sd], q);
 }
 
+namespace {
+// g_logs_fwht: erasure_logs* always take the two transforms (rs_debug_erasure_logs_check)
+std::atomic<bool> g_logs_fwht{false};
+
+// eval_poly on an erasure indicator is the dyadic convolution er[i] = sum over erased j of
+// log[i ^ j] (mod 65535; log[0] = 65535 adds nothing): the 65536-point transform of the
+// indicator times log_walsh, transformed back, 65536 = 1 (mod 65535). A plan reads er at
+// positions below W = ceilPow2(end) only, so a small erased set is summed point by point
+// there (c4: 512 points x 64 terms, ~10 us, against ~1.1 ms for the two transforms on a
+// first call's critical path); entries past W stay 0. Values agree with the transforms' mod
+// 65535 (0 and 65535 are the same log to every consumer: exp[65535] = exp[0], add_mod).
+void erasure_logs_of(uint16_t *er, uint64_t trunc, uint64_t W) {
+  if (!g_logs_fwht.load(std::memory_order_relaxed)) {
+    std::vector<uint32_t> ind;
+    for (uint64_t j = 0; j < trunc; j++)
+      if (er[j]) ind.push_back(static_cast<uint32_t>(j));
+    if (W * ind.size() <= (1u << 21)) {
+      const uint16_t *lg = tables().log;
+      for (uint64_t i = 0; i < W; i++) {
+        uint64_t sum = 0;
+        for (uint32_t j : ind) sum += lg[i ^ j];
+        er[i] = static_cast<uint16_t>(sum % kModulus);
+      }
+      return;
+    }
+  }
+  eval_poly(er, trunc);
+}
+}  // namespace
+
+void set_erasure_logs_fwht(bool on) { g_logs_fwht.store(on); }
+
 void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *er) {
   const uint64_t C = ceil_pow2(m), end = C + k;
   std::memset(er, 0, kOrder * sizeof(uint16_t));
@@ -178,7 +211,7 @@ void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *er)
   for (uint64_t i = m; i < C; i++) er[i] = 1;
   for (uint64_t i = C; i < end; i++)
     if (!received[i]) er[i] = 1;
-  eval_poly(er, end);
+  erasure_logs_of(er, end, ceil_pow2(end));
 }
 
 void scalar_reconstruct(uint16_t *sym, const uint8_t *received, const uint16_t *er, uint64_t k, uint64_t m,
@@ -247,7 +280,7 @@ void erasure_logs_low(const uint8_t *received, uint64_t k, uint64_t m, uint16_t 
   for (uint64_t i = C; i < end; i++)
     if (!received[i]) er[i] = 1;  // missing recovery
   for (uint64_t i = end; i < W; i++) er[i] = 1;  // P's values past the code: unknown
-  eval_poly(er, W);
+  erasure_logs_of(er, W, W);
 }
 
 void scalar_reconstruct_low(uint16_t *sym, const uint8_t *received, const uint16_t *er, uint64_t k, uint64_t m) {

@@ -12,6 +12,7 @@
 // the reference's 4 x 16-entry nibble tables (mul_128, tables.zig:96-118) that
 // x86 pshufb needs; both compute mul16(x, log_m) (utilities.zig:5-8) exactly.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -103,7 +104,10 @@ void scalar_fft(uint16_t *s, uint64_t size, uint64_t trunc, uint64_t sd, bool qu
 // IFFT chunk truncations of the encode schedule (root.zig:143-166; D2 drops the last full chunk)
 std::vector<uint64_t> encode_chunk_truncs(uint64_t k, uint64_t m, bool quirk_d2);
 // root.zig:277-289: erasure flags for a received pattern -> evalPoly -> logs (65536 entries)
+// (entries [0, ceilPow2(C + k)) are evaluated; the rest stay 0)
 void erasure_logs(const uint8_t *received, uint64_t k, uint64_t m, uint16_t *out);
+// test hook: erasure_logs* take eval_poly's two transforms even for small erased sets
+void set_erasure_logs_fwht(bool on);
 // Table for an FFT/IFFT twiddle: XOR-only marker when log_m == 65535
 // (the engine's `log_m == gf.modulus` shortcut, Generic.zig:38,47,53,103,...).
 RsTab make_twiddle(uint32_t skew_index, bool quirk_d1);

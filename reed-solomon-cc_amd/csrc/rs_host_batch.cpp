@@ -1,5 +1,8 @@
 // rs_host_batch.cpp — host-resident batches (end to end through a persistent 2-slot
 // H2D -> kernel -> D2H ring per device) and their multi-GPU split.
+#include <utility>
+#include <vector>
+
 #include "rs_host.hpp"
 
 using namespace rs;
@@ -65,6 +68,25 @@ struct Pipeline {
 int host_slots() {
   const char *e = std::getenv("RS_AMD_HOST_SLOTS");
   return e && *e ? std::max(1, std::min(Pipeline::kMaxSlots, std::atoi(e))) : 2;
+}
+// A slice's present shards cross PCIe as one strided copy per run of present rows; a run
+// bridges gaps of up to RS_AMD_HOST_GAP missing rows (their bytes are copied too and never
+// read: the caller's arrays hold every row). Measured per copy command: DESIGN.md §6 e2e.
+uint64_t host_gap_rows() {
+  const char *e = std::getenv("RS_AMD_HOST_GAP");
+  return e && *e ? static_cast<uint64_t>(std::max(0, std::atoi(e))) : 0ull;
+}
+// [first, last) runs of present[0, rows) with gaps of <= gap missing rows bridged
+std::vector<std::pair<uint64_t, uint64_t>> present_runs(const uint8_t *present, uint64_t rows, uint64_t gap) {
+  std::vector<std::pair<uint64_t, uint64_t>> runs;
+  for (uint64_t j = 0; j < rows; j++) {
+    if (!present[j]) continue;
+    if (!runs.empty() && j - runs.back().second <= gap)
+      runs.back().second = j + 1;
+    else
+      runs.emplace_back(j, j + 1);
+  }
+  return runs;
 }
 uint64_t host_slice_bytes() {
   const char *e = std::getenv("RS_AMD_HOST_SLICE_MB");
@@ -184,23 +206,23 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
     if ((st = p.ensure(bytes, slots))) return st;
+    const uint64_t gap = host_gap_rows();
+    const auto runs_o = present_runs(present, k, gap), runs_r = present_runs(present + k, m, gap);
     auto slices = [&]() -> int {
       for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
         const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
         const uint64_t cnt = std::min(S, n - s0);
         hipStream_t q = p.st[slot];
         if (inject_host_failure(i)) return fail(RS_ERR_DEVICE, "injected host-batch failure");
-        // only the present shards cross PCIe
-        for (uint64_t j = 0; j < k; j++)
-          if (present[j])
-            HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + j * sb, k * sb,
-                              static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + j * sb, orig_stride, sb, cnt,
-                              hipMemcpyHostToDevice, q));
-        for (uint64_t j = 0; j < m; j++)
-          if (present[k + j])
-            HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + j * sb, m * sb,
-                              static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + j * sb, rec_stride, sb, cnt,
-                              hipMemcpyHostToDevice, q));
+        // only the present shards cross PCIe (and bridged gaps), one copy per run of rows
+        for (const auto &r : runs_o)
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + r.first * sb, k * sb,
+                            static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + r.first * sb, orig_stride,
+                            (r.second - r.first) * sb, cnt, hipMemcpyHostToDevice, q));
+        for (const auto &r : runs_r)
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + r.first * sb, m * sb,
+                            static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + r.first * sb, rec_stride,
+                            (r.second - r.first) * sb, cnt, hipMemcpyHostToDevice, q));
         int rc = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
                                           p.buf[slot][2], 0, flags, q);
         if (rc) return rc;

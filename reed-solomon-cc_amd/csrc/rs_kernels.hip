@@ -1452,38 +1452,58 @@ __device__ void fwht_lds(uint16_t *e, uint32_t m) {
 
 // per stripe: present[k+m] -> logs[W] (root.zig:277-289 + Generic.zig:200-215). low: the
 // low-rate layout of rs_gf.cpp erasure_logs_low (C = ceilPow2(k): originals [0, k), known
-// zeros [k, C), recovery [C, C + m), unknown [C + m, W), transform over W)
+// zeros [k, C), recovery [C, C + m), unknown [C + m, W), transform over W). A small erased set
+// (W x |set| <= 2^20) is summed point by point, logs[p] = sum over erased j of log[p ^ j] mod
+// 65535 (the dyadic convolution the two transforms evaluate, rs_gf.cpp erasure_logs_of: equal
+// mod 65535); larger sets take the transforms in LDS.
+__device__ __forceinline__ uint32_t erased_flag(const uint8_t *pr, uint32_t i, uint32_t k, uint32_t m, uint32_t C,
+                                                uint32_t W, uint32_t end, uint32_t low) {
+  if (low) {
+    if (i < k) return pr[i] ? 0u : 1u;
+    if (i >= C && i < end) return pr[k + i - C] ? 0u : 1u;
+    return i >= end && i < W ? 1u : 0u;
+  }
+  if (i < m) return pr[k + i] ? 0u : 1u;
+  if (i < C) return 1u;
+  return i < end ? (pr[i - C] ? 0u : 1u) : 0u;
+}
+
 __global__ __launch_bounds__(1024) void k_erasure_logs(const uint8_t *__restrict__ present, uint64_t present_stride,
                                                        uint32_t k, uint32_t m, uint32_t C, uint32_t W, uint32_t low,
                                                        const uint16_t *__restrict__ log_walsh,
+                                                       const uint16_t *__restrict__ log_t,
                                                        uint16_t *__restrict__ logs) {
   __shared__ uint16_t e[65536];
+  __shared__ uint32_t n_er;
   const uint8_t *pr = present + static_cast<uint64_t>(blockIdx.x) * present_stride;
-  const uint32_t end = low ? C + m : C + k;
-  for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x) {
-    uint16_t v = 0;
-    if (low) {
-      if (i < k) v = pr[i] ? 0 : 1;
-      else if (i >= C && i < end) v = pr[k + i - C] ? 0 : 1;
-      else if (i >= end && i < W) v = 1;
-    } else if (i < m) {
-      v = pr[k + i] ? 0 : 1;
-    } else if (i < C) {
-      v = 1;
-    } else if (i < end) {
-      v = pr[i - C] ? 0 : 1;
+  const uint32_t end = low ? C + m : C + k, trunc = low ? W : end;
+  uint16_t *out = logs + static_cast<uint64_t>(blockIdx.x) * W;
+  if (threadIdx.x == 0) n_er = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < trunc; i += blockDim.x)
+    if (erased_flag(pr, i, k, m, C, W, end, low)) e[atomicAdd(&n_er, 1u)] = static_cast<uint16_t>(i);
+  __syncthreads();
+  const uint32_t n = n_er;
+  if (static_cast<uint64_t>(W) * n <= (1u << 20)) {  // integer sums: the list's order does not matter
+    for (uint32_t p = threadIdx.x; p < W; p += blockDim.x) {
+      uint32_t sum = 0;  // n <= 2^20 / W <= 1024 terms: no overflow
+      for (uint32_t j = 0; j < n; j++) sum += log_t[p ^ e[j]];
+      out[p] = static_cast<uint16_t>(sum % 65535u);
     }
-    e[i] = v;
+    return;
   }
   __syncthreads();
-  fwht_lds(e, low ? W : end);
+  for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x)
+    e[i] = static_cast<uint16_t>(i < trunc ? erased_flag(pr, i, k, m, C, W, end, low) : 0u);
+  __syncthreads();
+  fwht_lds(e, trunc);
   for (uint32_t i = threadIdx.x; i < 65536; i += blockDim.x) {
     const uint32_t prod = static_cast<uint32_t>(e[i]) * log_walsh[i];
     e[i] = static_cast<uint16_t>(add_mod_d(prod & 0xFFFF, prod >> 16));
   }
   __syncthreads();
   fwht_lds(e, 65536);
-  for (uint32_t p = threadIdx.x; p < W; p += blockDim.x) logs[static_cast<uint64_t>(blockIdx.x) * W + p] = e[p];
+  for (uint32_t p = threadIdx.x; p < W; p += blockDim.x) out[p] = e[p];
 }
 
 __device__ __forceinline__ uint32_t mul16_d(uint32_t x, uint32_t lm, const uint16_t *exp, const uint16_t *log) {
@@ -2010,7 +2030,7 @@ hipError_t launch_pattern_plan_impl(const uint8_t *d_present, uint64_t present_s
   for (uint64_t s0 = 0; s0 < n; s0 += 65535) {
     const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
     hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, d_present + s0 * present_stride,
-                       present_stride, k, m, C, W, low ? 1u : 0u, d_log_walsh, logs + s0 * W);
+                       present_stride, k, m, C, W, low ? 1u : 0u, d_log_walsh, d_log, logs + s0 * W);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -2867,7 +2887,7 @@ hipError_t launch_fdec_plan(const uint8_t *present, uint64_t present_stride, uin
   for (uint64_t s0 = 0; e == hipSuccess && s0 < n; s0 += 65535) {
     const uint32_t cnt = static_cast<uint32_t>(std::min<uint64_t>(65535, n - s0));
     hipLaunchKernelGGL(k_erasure_logs, dim3(cnt), dim3(1024), 0, s, trimmed + s0 * (k + m), static_cast<uint64_t>(k + m),
-                       k, m, C, W, 0u, d_log_walsh, logs + s0 * W);
+                       k, m, C, W, 0u, d_log_walsh, d_log, logs + s0 * W);
     e = hipGetLastError();
   }
   if (e != hipSuccess) return e;

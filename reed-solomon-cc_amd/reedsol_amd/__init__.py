@@ -92,6 +92,7 @@ def lib():
         "rs_last_kernels": (C.c_char_p, []),
         "rs_debug_fail_alloc": (C.c_int64, [C.c_int64]),
         "rs_debug_release_caches": (C.c_int, [vp]),
+        "rs_debug_erasure_logs_check": (C.c_int64, [C.c_uint64, C.c_uint64, vp, C.c_int]),
         "rs_debug_fft_stamps": (C.c_int, [vp, u64]),
         "rs_jit_stats": (C.c_int, [vp, vp, vp]),
         "rs_fft_compile_check": (C.c_int, [u64, u64, u32, vp, vp, vp]),
@@ -431,6 +432,13 @@ def reconstruct_warm(k, m, shard_bytes, present, flags: int = FLAG_CORRECTED) ->
     launch compiled and loaded), blocking; include/reedsol.h rs_reconstruct_warm."""
     pres = (C.c_uint8 * (k + m))(*[1 if p else 0 for p in present])
     _check(lib().rs_reconstruct_warm(k, m, shard_bytes, pres, flags))
+
+
+def debug_erasure_logs_check(k: int, m: int, received, low: bool = False) -> int:
+    """Positions where the library's point-by-point erasure locators differ (mod 65535) from
+    evalPoly's two transforms for one received pattern (host only; include/reedsol.h)."""
+    buf = (C.c_uint8 * len(received))(*[1 if r else 0 for r in received])
+    return int(lib().rs_debug_erasure_logs_check(k, m, buf, 1 if low else 0))
 
 
 def debug_fail_alloc(n: int) -> int:

@@ -352,9 +352,13 @@ def test_repeatable_and_nan_free_of_state():
     assert (gpu_encode(k, m, d) == gpu_encode(k, m, d)).all()
 
 
-@pytest.mark.parametrize("pinned", [True, False])
-def test_host_batch_pipeline(oracle, pinned):
-    """rs_encode_batch_host / rs_reconstruct_batch_host (H2D -> kernel -> D2H ring) == oracle."""
+@pytest.mark.parametrize("pinned,gap", [(True, None), (False, None), (True, "1"), (True, "64")])
+def test_host_batch_pipeline(oracle, monkeypatch, pinned, gap):
+    """rs_encode_batch_host / rs_reconstruct_batch_host (H2D -> kernel -> D2H ring) == oracle;
+    gap: RS_AMD_HOST_GAP, missing rows bridged inside one copy of present rows (their bytes
+    cross PCIe and are never read), here with missing data and recovery rows."""
+    if gap is not None:
+        monkeypatch.setenv("RS_AMD_HOST_GAP", gap)
     k, m, sb, n = 10, 4, 1 << 16, 37  # several pipeline slices at 256 MiB / (k*sb) = 409 stripes? -> force small
     data = torch.from_numpy(splitmix_bytes(77, n * k * sb).reshape(n, k, sb))
     if pinned:
@@ -365,11 +369,11 @@ def test_host_batch_pipeline(oracle, pinned):
     R.encode_batch_host(k, m, data, par)
     exp = oracle.encode_batch(k, m, data.numpy(), threads=4)
     assert (par.numpy() == exp).all()
-    present = [0, 1, 0, 1, 1, 1, 1, 0, 1, 1] + [1, 1, 1, 1]
-    missing = [i for i in range(k) if not present[i]]
-    out = torch.zeros((n, len(missing), sb), dtype=torch.uint8)
-    R.reconstruct_batch_host(k, m, present, data, par, out)
-    assert (out.numpy() == data.numpy()[:, missing]).all()
+    for present in ([0, 1, 0, 1, 1, 1, 1, 0, 1, 1] + [1, 1, 1, 1], [0, 1, 0, 1, 1, 1, 1, 0, 1, 1] + [1, 0, 1, 1]):
+        missing = [i for i in range(k) if not present[i]]
+        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8)
+        R.reconstruct_batch_host(k, m, present, data, par, out)
+        assert (out.numpy() == data.numpy()[:, missing]).all()
 
 
 @pytest.mark.parametrize("devices", [None, [0, 0], [0, 0, 0]])

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--shard-bytes", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=1024)
     ap.add_argument("--erase", type=str, default="0,1,2,3", help="erased indices, or N:first:step")
+    ap.add_argument("--rec-erase", type=str, default="", help="lost recovery rows N:first (indices into [0, m))")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--nv", type=str, default="1,2,4")
@@ -43,6 +44,10 @@ def main():
         raise SystemExit(f"--erase names shards outside [0, {k}): {erase}")
     e = len(erase)
     present = [0 if i in erase else 1 for i in range(k)] + [1] * m
+    if args.rec_erase:
+        cnt, first = (int(x) for x in args.rec_erase.split(":"))
+        for r in range(first, min(m, first + cnt)):
+            present[k + r] = 0
     dev = torch.device("cuda:0")
     data = torch.randint(0, 256, (n, k, sb), dtype=torch.uint8, device=dev)
     parity = torch.empty((n, m, sb), dtype=torch.uint8, device=dev)
