@@ -71,17 +71,18 @@ int host_slots() {
 }
 // A slice's present shards cross PCIe as one strided copy per run of present rows; a run
 // bridges gaps of up to RS_AMD_HOST_GAP missing rows (their bytes are copied too and never
-// read: the caller's arrays hold every row). Measured per copy command: DESIGN.md §6 e2e.
-uint64_t host_gap_rows() {
+// read: the caller's arrays hold every row); -1: one copy per row (round 5, measurement
+// baseline). Measured: DESIGN.md §6 e2e.
+int64_t host_gap_rows() {
   const char *e = std::getenv("RS_AMD_HOST_GAP");
-  return e && *e ? static_cast<uint64_t>(std::max(0, std::atoi(e))) : 0ull;
+  return e && *e ? std::max(-1, std::atoi(e)) : 0;
 }
 // [first, last) runs of present[0, rows) with gaps of <= gap missing rows bridged
-std::vector<std::pair<uint64_t, uint64_t>> present_runs(const uint8_t *present, uint64_t rows, uint64_t gap) {
+std::vector<std::pair<uint64_t, uint64_t>> present_runs(const uint8_t *present, uint64_t rows, int64_t gap) {
   std::vector<std::pair<uint64_t, uint64_t>> runs;
   for (uint64_t j = 0; j < rows; j++) {
     if (!present[j]) continue;
-    if (!runs.empty() && j - runs.back().second <= gap)
+    if (!runs.empty() && gap >= 0 && j - runs.back().second <= static_cast<uint64_t>(gap))
       runs.back().second = j + 1;
     else
       runs.emplace_back(j, j + 1);
@@ -206,7 +207,7 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
     if ((st = p.ensure(bytes, slots))) return st;
-    const uint64_t gap = host_gap_rows();
+    const int64_t gap = host_gap_rows();
     const auto runs_o = present_runs(present, k, gap), runs_r = present_runs(present + k, m, gap);
     auto slices = [&]() -> int {
       for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {

@@ -26,7 +26,9 @@ def main():
     ap.add_argument("--erase", type=str, default="0,1,2,3")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pageable-stripes", type=int, default=128)
+    ap.add_argument("--var", type=str, default="", help="NAME=v1,v2: env values alternated rep by rep in one process")
     a = ap.parse_args()
+    vname, vvals = (a.var.split("=", 1)[0], a.var.split("=", 1)[1].split(",")) if a.var else ("", [None])
     k, m, sb = a.k, a.m, a.shard_bytes
     erase = [int(x) for x in a.erase.split(",") if x]
     present = [0 if i in erase else 1 for i in range(k)] + [1] * m
@@ -40,22 +42,29 @@ def main():
             data, par, out = data.pin_memory(), par.pin_memory(), out.pin_memory()
         R.encode_batch_host(k, m, data[:1], par[:1])  # plan + warmup
         R.reconstruct_batch_host(k, m, present, data[:1], par[:1], out[:1])
-        te, tr = [], []
+        te, tr = {v: [] for v in vvals}, {v: [] for v in vvals}
+        ok = True
         for _ in range(a.reps):
-            t0 = time.perf_counter()
-            R.encode_batch_host(k, m, data, par)
-            te.append(time.perf_counter() - t0)
-            t0 = time.perf_counter()
-            R.reconstruct_batch_host(k, m, present, data, par, out)
-            tr.append(time.perf_counter() - t0)
-        ok = bool(torch.equal(out, data[:, erase]))
+            for v in vvals:
+                if v is not None:
+                    os.environ[vname] = v
+                t0 = time.perf_counter()
+                R.encode_batch_host(k, m, data, par)
+                te[v].append(time.perf_counter() - t0)
+                out.zero_()
+                t0 = time.perf_counter()
+                R.reconstruct_batch_host(k, m, present, data, par, out)
+                tr[v].append(time.perf_counter() - t0)
+                ok = ok and bool(torch.equal(out, data[:, erase]))
         gib = k * sb * n / 2**30
-        res[mode] = {"stripes": n, "encode_GiBps": round(gib / min(te), 2),
-                     "reconstruct_GiBps": round(gib / min(tr), 2),
-                     "encode_pcie_GBps": round((k + m) * sb * n / min(te) / 1e9, 2),
-                     "reconstruct_pcie_GBps": round((k + len(erase)) * sb * n / min(tr) / 1e9, 2),
-                     "verified": ok}
-        print(json.dumps({mode: res[mode]}), flush=True)
+        for v in vvals:
+            key = mode if v is None else f"{mode} {vname}={v}"
+            res[key] = {"stripes": n, "encode_GiBps": round(gib / min(te[v]), 2),
+                        "reconstruct_GiBps": round(gib / min(tr[v]), 2),
+                        "encode_pcie_GBps": round((k + m) * sb * n / min(te[v]) / 1e9, 2),
+                        "reconstruct_pcie_GBps": round((k + len(erase)) * sb * n / min(tr[v]) / 1e9, 2),
+                        "verified": ok}
+            print(json.dumps({key: res[key]}), flush=True)
     print(json.dumps(res))
 
 
