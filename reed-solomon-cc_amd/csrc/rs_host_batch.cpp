@@ -38,7 +38,7 @@ struct Pipeline {
   int ensure(const uint64_t bytes[3], int want) {
     for (int i = 0; i < want; i++)
       if (!st[i]) HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
-    bool grow = want != slots;
+    bool grow = want > slots;  // fewer slots wanted: the call uses the first `want`
     for (int j = 0; j < 3; j++) grow = grow || bytes[j] > cap[j];
     if (!grow) return RS_OK;
     for (int i = 0; i < kMaxSlots; i++)
@@ -51,7 +51,7 @@ struct Pipeline {
     for (int i = 0; i < want; i++)
       for (int j = 0; j < 3; j++)
         if (cap[j]) HIP_TRY(dev_malloc(&buf[i][j], cap[j]));
-    slots = want;
+    slots = std::max(slots, want);
     return RS_OK;
   }
   int finish() {
