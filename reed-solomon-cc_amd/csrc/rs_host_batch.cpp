@@ -1,5 +1,6 @@
 // rs_host_batch.cpp — host-resident batches (end to end through a persistent 2-slot
 // H2D -> kernel -> D2H ring per device) and their multi-GPU split.
+#include <cstdint>
 #include <utility>
 #include <vector>
 
@@ -92,6 +93,24 @@ std::vector<std::pair<uint64_t, uint64_t>> present_runs(const uint8_t *present, 
 uint64_t host_slice_bytes() {
   const char *e = std::getenv("RS_AMD_HOST_SLICE_MB");
   return (e && *e ? static_cast<uint64_t>(std::max(1, std::atoi(e))) : 256ull) << 20;
+}
+// Stripes per reconstruct slice: the default 256 MiB, widened (up to 1 GiB) until the narrowest
+// run's copy moves >= 8 MiB — c4 with every third data shard lost copies 2-row runs of 256 KiB
+// shards: 46.7 / 48.9 / 49.3 GiB/s at 256 / 512 / 1024 MiB slices, where RS(10,4)'s 6-row runs of
+// 1 MiB shards want 256 (50.0 / 49.3 / 47.8; profiles/r06/e2e/slice/). RS_AMD_HOST_SLICE_MB fixes it.
+uint64_t reconstruct_slice_stripes(uint64_t n, uint64_t stripe_bytes, uint64_t sb,
+                                   const std::vector<std::pair<uint64_t, uint64_t>> &runs) {
+  uint64_t S = std::max<uint64_t>(1, host_slice_bytes() / stripe_bytes);
+  const char *e = std::getenv("RS_AMD_HOST_SLICE_MB");
+  if (!(e && *e)) {
+    uint64_t narrow = UINT64_MAX;
+    for (const auto &r : runs) narrow = std::min(narrow, (r.second - r.first) * sb);
+    if (narrow != UINT64_MAX) {
+      const uint64_t want = ((8ull << 20) + narrow - 1) / narrow;
+      S = std::max(S, std::min(want, std::max<uint64_t>(1, (1ull << 30) / stripe_bytes)));
+    }
+  }
+  return std::min(S, n);
 }
 
 // Every slot stream is drained before a host-batch call returns, also after an error:
@@ -201,14 +220,16 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
     if (out_stride == 0) out_stride = e * sb;
     int dev;
     if ((st = current_device(&dev))) return st;
-    const uint64_t S = std::max<uint64_t>(1, std::min<uint64_t>(n, host_slice_bytes() / (k * sb)));
+    const int64_t gap = host_gap_rows();
+    const auto runs_o = present_runs(present, k, gap), runs_r = present_runs(present + k, m, gap);
+    auto runs_all = runs_o;
+    runs_all.insert(runs_all.end(), runs_r.begin(), runs_r.end());
+    const uint64_t S = reconstruct_slice_stripes(n, k * sb, sb, runs_all);
     const int slots = host_slots();
     Pipeline &p = Pipelines::of(dev);
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
     if ((st = p.ensure(bytes, slots))) return st;
-    const int64_t gap = host_gap_rows();
-    const auto runs_o = present_runs(present, k, gap), runs_r = present_runs(present + k, m, gap);
     auto slices = [&]() -> int {
       for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
         const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
