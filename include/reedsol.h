@@ -153,7 +153,9 @@ int rs_reconstruct_batch_dev_patterns(uint64_t original_count, uint64_t recovery
  * A reconstruct reads only the present shards: one copy per run of consecutive present
  * rows (RS_AMD_HOST_GAP=n also copies gaps of up to n missing rows, bytes never read),
  * in slices of 256 MiB (RS_AMD_HOST_SLICE_MB) widened up to 1 GiB while the narrowest
- * run's copy would move less than 8 MiB. The ring's device buffers persist per device. */
+ * run's copy would move less than 8 MiB. Ring copies use the 2D copy form (faster than the
+ * 1D one from pinned memory; RS_AMD_HOST_COPY2D=0 reverts). The ring's device buffers persist
+ * per device. */
 int rs_encode_batch_host(uint64_t original_count, uint64_t recovery_count, size_t shard_bytes, uint64_t n_stripes,
                          const void *h_original, uint64_t original_stripe_stride, void *h_recovery,
                          uint64_t recovery_stripe_stride, uint32_t flags);
