@@ -1,6 +1,8 @@
 // rs_host_batch.cpp — host-resident batches (end to end through a persistent 2-slot
 // H2D -> kernel -> D2H ring per device) and their multi-GPU split.
 #include <cstdint>
+#include <cstring>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -32,6 +34,62 @@ hipError_t copy_rows(void *dst, uint64_t dst_stride, const void *src, uint64_t s
   return hipMemcpy2DAsync(dst, dst_stride, src, src_stride, row_bytes, rows, kind, s);
 }
 
+// Pageable host buffers go through the ring's own pinned staging (RS_AMD_HOST_STAGE, default
+// on): host threads copy a slice's rows into it while the previous slice is on PCIe, and the
+// device copies run from pinned memory in the 2D form; the runtime's own pageable path stages
+// through a smaller buffer one copy at a time.
+bool host_stage_on() {
+  const char *e = std::getenv("RS_AMD_HOST_STAGE");
+  return !(e && *e == '0');
+}
+bool is_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+         a.type == hipMemoryTypeUnified;
+}
+int stage_threads() {
+  const char *e = std::getenv("RS_AMD_HOST_THREADS");
+  const int hw = static_cast<int>(std::thread::hardware_concurrency());
+  return e && *e ? std::max(1, std::min(64, std::atoi(e))) : std::max(1, std::min(16, hw));
+}
+// strided host-to-host copies (rows of `w` bytes), split into <= 4 MiB pieces over host threads
+struct CopyJob {
+  uint8_t *d;
+  uint64_t ds;
+  const uint8_t *s;
+  uint64_t ss, w, rows;
+};
+void host_copy(const std::vector<CopyJob> &jobs) {
+  struct Piece {
+    uint8_t *d;
+    const uint8_t *s;
+    uint64_t len;
+  };
+  std::vector<Piece> pieces;
+  for (const CopyJob &j : jobs)
+    for (uint64_t r = 0; r < j.rows; r++)
+      for (uint64_t o = 0; o < j.w; o += 4ull << 20)
+        pieces.push_back({j.d + r * j.ds + o, j.s + r * j.ss + o, std::min<uint64_t>(4ull << 20, j.w - o)});
+  const int T = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(stage_threads()), pieces.size()));
+  auto work = [&](int t) {
+    for (size_t i = static_cast<size_t>(t); i < pieces.size(); i += static_cast<size_t>(T))
+      std::memcpy(pieces[i].d, pieces[i].s, pieces[i].len);
+  };
+  if (T <= 1) {
+    if (T == 1) work(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+}
+
 // Per-device staging ring of the host-batch calls: `slots` slices, each on its own
 // stream (H2D -> kernel -> D2H in order; slices on different streams overlap both
 // PCIe directions with the kernels). Buffers and streams persist across calls and
@@ -43,6 +101,26 @@ struct Pipeline {
   hipStream_t st[kMaxSlots] = {};
   void *buf[kMaxSlots][3] = {};
   uint64_t cap[3] = {};
+  void *hst[kMaxSlots][3] = {};  // pinned host staging of pageable callers' slices
+  uint64_t hcap[3] = {};
+  int hslots = 0;
+  int ensure_stage(const uint64_t bytes[3], int want) {
+    bool grow = want > hslots;
+    for (int j = 0; j < 3; j++) grow = grow || bytes[j] > hcap[j];
+    if (!grow) return RS_OK;
+    for (int i = 0; i < kMaxSlots; i++)
+      for (int j = 0; j < 3; j++) {
+        if (hst[i][j]) HIP_TRY(hipHostFree(hst[i][j]));
+        hst[i][j] = nullptr;
+      }
+    hslots = 0;
+    for (int j = 0; j < 3; j++) hcap[j] = std::max(hcap[j], bytes[j]);
+    for (int i = 0; i < want; i++)
+      for (int j = 0; j < 3; j++)
+        if (hcap[j]) HIP_TRY(pinned_malloc(&hst[i][j], hcap[j]));
+    hslots = want;
+    return RS_OK;
+  }
   int ensure(const uint64_t bytes[3], int want) {
     for (int i = 0; i < want; i++)
       if (!st[i]) HIP_TRY(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
@@ -120,13 +198,6 @@ uint64_t reconstruct_slice_stripes(uint64_t n, uint64_t stripe_bytes, uint64_t s
   return std::min(S, n);
 }
 
-// Every slot stream is drained before a host-batch call returns, also after an error:
-// no copy into the caller's buffers (or out of them) outlives the call.
-int drain_after(Pipeline &p, int rc) {
-  const int fin = p.finish();
-  return rc ? rc : fin;
-}
-
 // Fault injection for the error-path test (the reference's checkAllAllocationFailures,
 // tests.zig:131-156, in spirit): RS_AMD_INJECT_HOST_FAIL=i fails slice i of a host batch.
 bool inject_host_failure(uint64_t slice) {
@@ -164,6 +235,13 @@ void rs::host::release_host_rings() {
       }
     p.slots = 0;
     for (int j = 0; j < 3; j++) p.cap[j] = 0;
+    for (int i = 0; i < Pipeline::kMaxSlots; i++)
+      for (int j = 0; j < 3; j++) {
+        if (p.hst[i][j]) (void)hipHostFree(p.hst[i][j]);
+        p.hst[i][j] = nullptr;
+      }
+    p.hslots = 0;
+    for (int j = 0; j < 3; j++) p.hcap[j] = 0;
     (void)hipSetDevice(cur);
   }
 }
@@ -189,22 +267,52 @@ int rs_encode_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, const vo
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, 0};
     if ((st = p.ensure(bytes, slots))) return st;
+    const bool stage = host_stage_on() && !(is_pinned(h_orig) && is_pinned(h_rec));
+    if (stage && (st = p.ensure_stage(bytes, slots))) return st;
+    uint64_t pend_s0[Pipeline::kMaxSlots] = {}, pend_cnt[Pipeline::kMaxSlots] = {};
+    // staged: a slot's previous slice is waited for and its parity copied out before the slot's
+    // staging buffers take the next slice
+    auto take_out = [&](int slot) {
+      if (!pend_cnt[slot]) return;
+      host_copy({{static_cast<uint8_t *>(h_rec) + pend_s0[slot] * rec_stride, rec_stride,
+                  static_cast<const uint8_t *>(p.hst[slot][1]), m * sb, m * sb, pend_cnt[slot]}});
+      pend_cnt[slot] = 0;
+    };
     auto slices = [&]() -> int {
       for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
         const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
         const uint64_t cnt = std::min(S, n - s0);
         hipStream_t q = p.st[slot];
         if (inject_host_failure(i)) return fail(RS_ERR_DEVICE, "injected host-batch failure");
-        HIP_TRY(copy_rows(p.buf[slot][0], k * sb, static_cast<const uint8_t *>(h_orig) + s0 * orig_stride,
-                          orig_stride, k * sb, cnt, hipMemcpyHostToDevice, q));
+        const uint8_t *src = static_cast<const uint8_t *>(h_orig) + s0 * orig_stride;
+        uint64_t src_stride = orig_stride;
+        if (stage) {
+          HIP_TRY(hipStreamSynchronize(q));
+          take_out(slot);
+          host_copy({{static_cast<uint8_t *>(p.hst[slot][0]), k * sb, src, orig_stride, k * sb, cnt}});
+          src = static_cast<const uint8_t *>(p.hst[slot][0]);
+          src_stride = k * sb;
+        }
+        HIP_TRY(copy_rows(p.buf[slot][0], k * sb, src, src_stride, k * sb, cnt, hipMemcpyHostToDevice, q));
         int rc = rs_encode_batch_dev(k, m, sb, cnt, p.buf[slot][0], 0, p.buf[slot][1], 0, flags, q);
         if (rc) return rc;
-        HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb,
-                          m * sb, cnt, hipMemcpyDeviceToHost, q));
+        if (stage) {
+          HIP_TRY(copy_rows(p.hst[slot][1], m * sb, p.buf[slot][1], m * sb, m * sb, cnt, hipMemcpyDeviceToHost, q));
+          pend_s0[slot] = s0;
+          pend_cnt[slot] = cnt;
+        } else {
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(h_rec) + s0 * rec_stride, rec_stride, p.buf[slot][1], m * sb,
+                            m * sb, cnt, hipMemcpyDeviceToHost, q));
+        }
       }
       return RS_OK;
     };
-    return drain_after(p, slices());
+    // every slot stream is drained before the call returns, also after an error: no copy into
+    // the caller's buffers (or out of them) outlives the call
+    const int rc = slices(), fin = p.finish();
+    if (stage && fin == RS_OK)
+      for (int slot = 0; slot < slots; slot++) take_out(slot);  // slices that completed, also before an error
+    return rc ? rc : fin;
   });
 }
 
@@ -237,30 +345,64 @@ int rs_reconstruct_batch_host(uint64_t k, uint64_t m, size_t sb, uint64_t n, con
     std::lock_guard<std::mutex> lk(p.mu);
     const uint64_t bytes[3] = {S * k * sb, S * m * sb, S * e * sb};
     if ((st = p.ensure(bytes, slots))) return st;
+    const bool stage = host_stage_on() && !(is_pinned(h_orig) && is_pinned(h_rec) && is_pinned(h_out));
+    if (stage && (st = p.ensure_stage(bytes, slots))) return st;
+    uint64_t pend_s0[Pipeline::kMaxSlots] = {}, pend_cnt[Pipeline::kMaxSlots] = {};
+    auto take_out = [&](int slot) {
+      if (!pend_cnt[slot]) return;
+      host_copy({{static_cast<uint8_t *>(h_out) + pend_s0[slot] * out_stride, out_stride,
+                  static_cast<const uint8_t *>(p.hst[slot][2]), e * sb, e * sb, pend_cnt[slot]}});
+      pend_cnt[slot] = 0;
+    };
     auto slices = [&]() -> int {
       for (uint64_t s0 = 0, i = 0; s0 < n; s0 += S, i++) {
         const int slot = static_cast<int>(i % static_cast<uint64_t>(slots));
         const uint64_t cnt = std::min(S, n - s0);
         hipStream_t q = p.st[slot];
         if (inject_host_failure(i)) return fail(RS_ERR_DEVICE, "injected host-batch failure");
+        const uint8_t *so = static_cast<const uint8_t *>(h_orig) + s0 * orig_stride;
+        const uint8_t *sr = static_cast<const uint8_t *>(h_rec) + s0 * rec_stride;
+        uint64_t sos = orig_stride, srs = rec_stride;
+        if (stage) {  // the present rows into the slot's staging, in the device layout
+          HIP_TRY(hipStreamSynchronize(q));
+          take_out(slot);
+          std::vector<CopyJob> jobs;
+          uint8_t *ho = static_cast<uint8_t *>(p.hst[slot][0]), *hr = static_cast<uint8_t *>(p.hst[slot][1]);
+          for (const auto &r : runs_o)
+            jobs.push_back({ho + r.first * sb, k * sb, so + r.first * sb, orig_stride, (r.second - r.first) * sb, cnt});
+          for (const auto &r : runs_r)
+            jobs.push_back({hr + r.first * sb, m * sb, sr + r.first * sb, rec_stride, (r.second - r.first) * sb, cnt});
+          host_copy(jobs);
+          so = ho;
+          sr = hr;
+          sos = k * sb;
+          srs = m * sb;
+        }
         // only the present shards cross PCIe (and bridged gaps), one copy per run of rows
         for (const auto &r : runs_o)
-          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + r.first * sb, k * sb,
-                            static_cast<const uint8_t *>(h_orig) + s0 * orig_stride + r.first * sb, orig_stride,
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][0]) + r.first * sb, k * sb, so + r.first * sb, sos,
                             (r.second - r.first) * sb, cnt, hipMemcpyHostToDevice, q));
         for (const auto &r : runs_r)
-          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + r.first * sb, m * sb,
-                            static_cast<const uint8_t *>(h_rec) + s0 * rec_stride + r.first * sb, rec_stride,
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(p.buf[slot][1]) + r.first * sb, m * sb, sr + r.first * sb, srs,
                             (r.second - r.first) * sb, cnt, hipMemcpyHostToDevice, q));
         int rc = rs_reconstruct_batch_dev(k, m, sb, cnt, present, p.buf[slot][0], 0, p.buf[slot][1], 0,
                                           p.buf[slot][2], 0, flags, q);
         if (rc) return rc;
-        HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb,
-                          e * sb, cnt, hipMemcpyDeviceToHost, q));
+        if (stage) {
+          HIP_TRY(copy_rows(p.hst[slot][2], e * sb, p.buf[slot][2], e * sb, e * sb, cnt, hipMemcpyDeviceToHost, q));
+          pend_s0[slot] = s0;
+          pend_cnt[slot] = cnt;
+        } else {
+          HIP_TRY(copy_rows(static_cast<uint8_t *>(h_out) + s0 * out_stride, out_stride, p.buf[slot][2], e * sb,
+                            e * sb, cnt, hipMemcpyDeviceToHost, q));
+        }
       }
       return RS_OK;
     };
-    return drain_after(p, slices());
+    const int rc = slices(), fin = p.finish();
+    if (stage && fin == RS_OK)
+      for (int slot = 0; slot < slots; slot++) take_out(slot);
+    return rc ? rc : fin;
   });
 }
 

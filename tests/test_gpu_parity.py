@@ -352,13 +352,19 @@ def test_repeatable_and_nan_free_of_state():
     assert (gpu_encode(k, m, d) == gpu_encode(k, m, d)).all()
 
 
-@pytest.mark.parametrize("pinned,gap", [(True, None), (False, None), (True, "1"), (True, "64")])
-def test_host_batch_pipeline(oracle, monkeypatch, pinned, gap):
+@pytest.mark.parametrize("pinned,gap,slice_mb,stage", [(True, None, None, None), (False, None, None, None),
+                                                       (True, "1", None, None), (True, "64", None, None),
+                                                       (False, None, "1", None), (False, "1", "2", None),
+                                                       (False, None, "1", "0")])
+def test_host_batch_pipeline(oracle, monkeypatch, pinned, gap, slice_mb, stage):
     """rs_encode_batch_host / rs_reconstruct_batch_host (H2D -> kernel -> D2H ring) == oracle;
     gap: RS_AMD_HOST_GAP, missing rows bridged inside one copy of present rows (their bytes
-    cross PCIe and are never read), here with missing data and recovery rows."""
-    if gap is not None:
-        monkeypatch.setenv("RS_AMD_HOST_GAP", gap)
+    cross PCIe and are never read), here with missing data and recovery rows. Pageable
+    buffers go through the ring's pinned staging (RS_AMD_HOST_STAGE=0: the runtime's path),
+    over many slices (RS_AMD_HOST_SLICE_MB) so both slots' staging is reused."""
+    for name, val in (("RS_AMD_HOST_GAP", gap), ("RS_AMD_HOST_SLICE_MB", slice_mb), ("RS_AMD_HOST_STAGE", stage)):
+        if val is not None:
+            monkeypatch.setenv(name, val)
     k, m, sb, n = 10, 4, 1 << 16, 37  # several pipeline slices at 256 MiB / (k*sb) = 409 stripes? -> force small
     data = torch.from_numpy(splitmix_bytes(77, n * k * sb).reshape(n, k, sb))
     if pinned:
@@ -394,25 +400,31 @@ def test_host_batch_multi_device(oracle, devices):
     assert (out.numpy() == data.numpy()[:, missing]).all()
 
 
+@pytest.mark.parametrize("pinned", [True, False])
 @pytest.mark.parametrize("op", ["encode", "reconstruct"])
-def test_host_batch_error_drains_slices(oracle, monkeypatch, op):
+def test_host_batch_error_drains_slices(oracle, monkeypatch, op, pinned):
     """A host batch whose 4th slice fails (fault injection, RS_AMD_INJECT_HOST_FAIL):
     the call returns the error only after the earlier slices' copies have landed
-    (every slot stream drained), and no later slice is written."""
+    (every slot stream drained; pageable: copied out of the staging), and no later slice is
+    written."""
     k, m, sb, n = 10, 4, 1 << 16, 9
     monkeypatch.setenv("RS_AMD_HOST_SLICE_MB", "1")  # 1 MiB / 640 KiB -> 1 stripe per slice
     monkeypatch.setenv("RS_AMD_INJECT_HOST_FAIL", "3")
-    data = torch.from_numpy(splitmix_bytes(91, n * k * sb).reshape(n, k, sb)).pin_memory()
+
+    def mem(t):
+        return t.pin_memory() if pinned else t
+
+    data = mem(torch.from_numpy(splitmix_bytes(91, n * k * sb).reshape(n, k, sb)))
     exp = oracle.encode_batch(k, m, data.numpy(), threads=4)
     if op == "encode":
-        out = torch.zeros((n, m, sb), dtype=torch.uint8).pin_memory()
+        out = mem(torch.zeros((n, m, sb), dtype=torch.uint8))
         st = R.lib().rs_encode_batch_host(k, m, sb, n, data.data_ptr(), 0, out.data_ptr(), 0, 0)
         want = exp
     else:
         present = np.array([0, 1, 0, 1, 1, 1, 1, 0, 1, 1] + [1, 1, 1, 1], np.uint8)
         missing = [i for i in range(k) if not present[i]]
-        par = torch.from_numpy(exp).pin_memory()
-        out = torch.zeros((n, len(missing), sb), dtype=torch.uint8).pin_memory()
+        par = mem(torch.from_numpy(exp))
+        out = mem(torch.zeros((n, len(missing), sb), dtype=torch.uint8))
         st = R.lib().rs_reconstruct_batch_host(k, m, sb, n, present.ctypes.data, data.data_ptr(), 0, par.data_ptr(), 0,
                                                out.data_ptr(), 0, 0)
         want = data.numpy()[:, missing]
