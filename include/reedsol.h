@@ -149,8 +149,8 @@ int rs_reconstruct_batch_dev_patterns(uint64_t original_count, uint64_t recovery
  * H2D -> kernel -> D2H pipeline on its own streams (PCIe full duplex overlapped
  * with compute) and returns when the results are in host memory. Pinned host
  * buffers (hipHostMalloc / hipHostRegister / torch pin_memory) run at PCIe rate;
- * pageable buffers are copied by host threads through the ring's own pinned staging
- * (RS_AMD_HOST_STAGE=0: the HIP runtime's pageable path instead).
+ * pageable buffers are copied by host threads (up to 16, RS_AMD_HOST_THREADS) through the
+ * ring's own pinned staging (RS_AMD_HOST_STAGE=0: the HIP runtime's pageable path instead).
  * A reconstruct reads only the present shards: one copy per run of consecutive present
  * rows (RS_AMD_HOST_GAP=n also copies gaps of up to n missing rows, bytes never read),
  * in slices of 256 MiB (RS_AMD_HOST_SLICE_MB) widened up to 1 GiB while the narrowest
